@@ -1,0 +1,145 @@
+"""ctypes view of the C ABI declared in include/cmpc.h.
+
+The product library is compressor-mpc_amd/cmpc/libcmpc.so (HIP, gfx950),
+built in-tree by compressor-mpc_amd/csrc/Makefile.  There is no CPU fallback:
+if the library is missing or cannot be loaded, load_library() raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcmpc.so")
+
+CMPC_MAX_INPUTS = 8
+CMPC_MAX_NV = 8
+CMPC_MAX_NS = 15
+CMPC_NWSR_MAX = 10
+
+CMPC_QP_OK = 0
+CMPC_QP_MAX_NWSR = 1
+CMPC_QP_INFEASIBLE = 2
+CMPC_QP_NOT_PD = 3
+
+CMPC_APPLY_MOVE = 1
+CMPC_TRACE = 2
+
+CMPC_KERNEL_BUILD = 0
+CMPC_KERNEL_ITERATE = 1
+
+
+class CmpcDims(ctypes.Structure):
+    _fields_ = [("ns", ctypes.c_int32), ("ndist", ctypes.c_int32),
+                ("nu_tot", ctypes.c_int32), ("nu", ctypes.c_int32),
+                ("ny", ctypes.c_int32), ("p", ctypes.c_int32), ("m", ctypes.c_int32),
+                ("delay", ctypes.c_int32 * CMPC_MAX_INPUTS),
+                ("S", ctypes.c_int32), ("B", ctypes.c_int32)]
+
+    @classmethod
+    def from_config(cls, cfg, B: int) -> "CmpcDims":
+        d = cls()
+        d.ns, d.ndist, d.nu_tot, d.nu, d.ny = cfg.ns, cfg.ndist, cfg.nu_tot, cfg.nu, cfg.ny
+        d.p, d.m, d.S, d.B = cfg.p, cfg.m, cfg.S, B
+        for i, v in enumerate(cfg.delays):
+            d.delay[i] = v
+        return d
+
+
+class CmpcLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("nd", "n_delay_states", "naug", "nobs", "ntot", "nV", "nuo", "nVo",
+                 "off_A", "off_B", "off_C", "off_f", "off_x", "off_y", "rec_len")]
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def uptr(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def bptr(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+# Every symbol include/cmpc.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "cmpc_layout_of", "cmpc_create", "cmpc_destroy", "cmpc_set_stream",
+    "cmpc_last_error", "cmpc_get_layout", "cmpc_set_weights", "cmpc_set_constraints",
+    "cmpc_set_reference", "cmpc_set_state", "cmpc_get_state", "cmpc_upload_lin",
+    "cmpc_lin_device", "cmpc_build", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
+    "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
+    "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
+    "cmpc_plant_output", "cmpc_plant_lin_record",
+)
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libcmpc.so.  Raises (never falls back) if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} not found: build it with `make -C compressor-mpc_amd/csrc` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    c_void = ctypes.c_void_p
+    i32, u32, dbl = ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
+    sig = {
+        "cmpc_layout_of": ([P(CmpcDims), P(CmpcLayout)], ctypes.c_int),
+        "cmpc_create": ([P(c_void), P(CmpcDims), ctypes.c_int], ctypes.c_int),
+        "cmpc_destroy": ([c_void], ctypes.c_int),
+        "cmpc_set_stream": ([c_void, c_void], ctypes.c_int),
+        "cmpc_last_error": ([], ctypes.c_char_p),
+        "cmpc_get_layout": ([c_void, P(CmpcLayout)], ctypes.c_int),
+        "cmpc_set_weights": ([c_void, ctypes.c_int, P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_set_constraints": ([c_void, ctypes.c_int, P(dbl), P(dbl), P(dbl), P(dbl)],
+                                 ctypes.c_int),
+        "cmpc_set_reference": ([c_void, ctypes.c_int, P(dbl)], ctypes.c_int),
+        "cmpc_set_state": ([c_void, P(dbl), P(dbl), P(u32)], ctypes.c_int),
+        "cmpc_get_state": ([c_void, P(dbl), P(dbl), P(u32)], ctypes.c_int),
+        "cmpc_upload_lin": ([c_void, P(dbl)], ctypes.c_int),
+        "cmpc_lin_device": ([c_void], c_void),
+        "cmpc_build": ([c_void], ctypes.c_int),
+        "cmpc_init_warmstart": ([c_void], ctypes.c_int),
+        "cmpc_iterate": ([c_void, ctypes.c_int, u32], ctypes.c_int),
+        "cmpc_step": ([c_void, ctypes.c_int, u32], ctypes.c_int),
+        "cmpc_synchronize": ([c_void], ctypes.c_int),
+        "cmpc_download": ([c_void, P(dbl), P(i32), P(i32)], ctypes.c_int),
+        "cmpc_download_qp": ([c_void, P(dbl), P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_download_trace": ([c_void, P(ctypes.c_uint8), P(i32)], ctypes.c_int),
+        "cmpc_enable_timing": ([c_void, ctypes.c_int], ctypes.c_int),
+        "cmpc_kernel_time": ([c_void, ctypes.c_int, P(dbl), P(ctypes.c_int64)], ctypes.c_int),
+        "cmpc_plant_dims": ([ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int),
+                             P(ctypes.c_int)], ctypes.c_int),
+        "cmpc_plant_default": ([ctypes.c_int, P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_plant_output": ([ctypes.c_int, P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_plant_lin_record": ([ctypes.c_int, dbl, dbl, dbl, P(dbl), P(dbl), P(i32), P(i32),
+                                   P(CmpcDims), P(dbl)], ctypes.c_int),
+    }
+    for name, (argtypes, restype) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "cmpc call"):
+    if rc != 0:
+        msg = load_library().cmpc_last_error()
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

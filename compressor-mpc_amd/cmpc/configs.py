@@ -1,0 +1,145 @@
+"""Reference controller configurations (compile-time constants of the reference,
+restated as run-time dimensions).
+
+Sources (katie-jones/compressor-mpc):
+  include/parallel_compressors_constants.h:68-94   (parallel plant)
+  include/serial_compressors_constants.h:82-110    (serial plant)
+  include/common-variables.h:20-112                (controller type selection)
+  include/parallel_compressors.h:13-23, include/serial_compressors.h:13-30
+
+A configuration fixes, per sub-controller s:
+  input_order[s]  ControlInputIndices of its AugmentedLinearizedSystem (own
+                  inputs first, then the other controllers' inputs)
+  out_idx[s]      ControlledOutputIndices
+and the shared dims (ns, ndist, nu_tot, nu, ny, p, m, delays).
+"""
+from dataclasses import dataclass, field
+from typing import List
+
+PLANT_PARALLEL = 0
+PLANT_SERIAL = 1
+
+# Delays = ConstexprArray<0, 40, 0, 40>; n_disturbance_states = 4
+REF_DELAYS = (0, 40, 0, 40)
+REF_NDIST = 4
+REF_P = 100
+REF_M = 2
+REF_TS = 0.05  # sampling time of results/*.dat records
+
+
+@dataclass
+class ControllerConfig:
+    plant: int
+    controller: str                 # "cent" | "coop" | "ncoop"
+    ns: int
+    nu_tot: int
+    nu: int
+    ny: int
+    input_order: List[List[int]]    # per sub-controller
+    out_idx: List[List[int]]        # per sub-controller
+    delays: tuple = REF_DELAYS
+    ndist: int = REF_NDIST
+    p: int = REF_P
+    m: int = REF_M
+
+    @property
+    def S(self) -> int:
+        return len(self.input_order)
+
+    @property
+    def nV(self) -> int:
+        return self.m * self.nu
+
+    @property
+    def nVo(self) -> int:
+        return self.m * (self.nu_tot - self.nu)
+
+    def own_inputs(self, s: int) -> List[int]:
+        """Plant control-input indices owned by sub-controller s
+        (ControlInputIndexType = first nu entries of ControlInputIndices)."""
+        return self.input_order[s][: self.nu]
+
+    def with_horizon(self, p: int, m: int = None) -> "ControllerConfig":
+        c = ControllerConfig(**{k: getattr(self, k) for k in self.__dataclass_fields__})
+        c.p = p
+        if m is not None:
+            c.m = m
+        return c
+
+
+def reference_config(plant: str, controller: str, p: int = REF_P, m: int = REF_M) -> ControllerConfig:
+    """plant: 'par'|'ser'; controller: 'cent'|'coop'|'ncoop'."""
+    if plant in ("par", "parallel"):
+        pl, ns = PLANT_PARALLEL, 11
+        ctrl_out = [0, 1, 3]                       # ControlledOutputIndices
+        nc_out = [[0, 3], [1, 3]]                  # NCControlledOutputIndices1/2
+    elif plant in ("ser", "serial"):
+        pl, ns = PLANT_SERIAL, 10
+        ctrl_out = [0, 1, 2, 3]                    # NullIndexArray<4>
+        nc_out = [[0, 1], [2, 3]]                  # NCControlledOutputIndices1/2
+    else:
+        raise ValueError(plant)
+    ci1, ci2 = [0, 1, 2, 3], [2, 3, 0, 1]          # ControlInputIndices1/2
+    if controller in ("cent", "centralized"):
+        return ControllerConfig(pl, "cent", ns, 4, 4, len(ctrl_out), [ci1], [ctrl_out], p=p, m=m)
+    if controller in ("coop", "cooperative"):
+        return ControllerConfig(pl, "coop", ns, 4, 2, len(ctrl_out), [ci1, ci2],
+                                [ctrl_out, ctrl_out], p=p, m=m)
+    if controller in ("ncoop", "noncoop"):
+        return ControllerConfig(pl, "ncoop", ns, 4, 2, 2, [ci1, ci2], nc_out, p=p, m=m)
+    raise ValueError(controller)
+
+
+@dataclass
+class SetupFile:
+    """Run parameters of a reference setup file (setup/setup-<ctrl>-<plant>),
+    parsed like include/read_files.h:13-81 (key line, then value lines)."""
+    n_iterations: int = 1
+    n_timing_iterations: int = 1
+    yref: List[float] = field(default_factory=list)
+    uwt: List[float] = field(default_factory=list)     # n_control_inputs^2
+    ywt: List[List[float]] = field(default_factory=list)  # one ny x ny block per sub-controller
+    constraints_lower: List[float] = field(default_factory=list)
+    constraints_upper: List[float] = field(default_factory=list)
+    rate_lower: List[float] = field(default_factory=list)
+    rate_upper: List[float] = field(default_factory=list)
+
+    KEYS = ("n-iterations", "n-timing-iterations", "folder-name", "output-filename",
+            "yref", "uwt", "ywt", "constraints-lower", "constraints-upper",
+            "constraints-rate-lower", "constraints-rate-upper", "simulation")
+
+    @classmethod
+    def parse(cls, text: str, cfg: ControllerConfig) -> "SetupFile":
+        blocks, key = {}, None
+        for line in text.splitlines():
+            s = line.strip()
+            if not s or s.startswith("#"):
+                continue
+            tok = s.split()
+            if tok[0] in cls.KEYS:
+                key = tok[0]
+                blocks.setdefault(key, [])
+                continue
+            if key is None:
+                raise RuntimeError(f"Error reading setup file at line: {line!r}")
+            blocks[key].extend(tok)
+        num = lambda k: [float(t) for t in blocks.get(k, [])]
+        out = cls()
+        out.n_iterations = int(num("n-iterations")[0]) if "n-iterations" in blocks else 1
+        out.n_timing_iterations = (int(num("n-timing-iterations")[0])
+                                   if "n-timing-iterations" in blocks else out.n_iterations)
+        out.yref = num("yref")
+        out.uwt = num("uwt")
+        yw = num("ywt")
+        blk = cfg.ny * cfg.ny
+        if len(yw) == blk:
+            out.ywt = [yw] * cfg.S
+        elif len(yw) == blk * cfg.S:
+            out.ywt = [yw[i * blk:(i + 1) * blk] for i in range(cfg.S)]
+        else:
+            raise RuntimeError(f"ywt: expected {blk} or {blk * cfg.S} numbers, got {len(yw)}")
+        out.constraints_lower = num("constraints-lower")
+        out.constraints_upper = num("constraints-upper")
+        out.rate_lower = num("constraints-rate-lower")
+        out.rate_upper = num("constraints-rate-upper")
+        return out

@@ -1,0 +1,182 @@
+/*
+ * cmpc.h — C ABI of the MI355X-native condensed-QP hot path of
+ * katie-jones/compressor-mpc (cooperative / non-cooperative / centralized
+ * linear-time-varying MPC).
+ *
+ * Plain C, POD arguments only, int status returns (0 = ok, <0 = error; the
+ * message is in cmpc_last_error()).  One context per (device, stream, host
+ * thread); a context is not thread-safe.  All batched device buffers are
+ * owned by the library; host arrays are owned by the caller.
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference root):
+ *
+ *   cmpc_create            MpcQpSolver ctor  libs/mpc_qp_solver.cc:3-14,
+ *                          DistributedController ctor libs/distributed_controller.cc:6-22,
+ *                          NerveCenter ctor include/nerve_center.h:89-95
+ *   cmpc_set_weights       MpcQpSolver::SetWeights include/mpc_qp_solver.h:62-80,
+ *                          NerveCenter::SetWeights include/nerve_center.h:107-116
+ *   cmpc_set_constraints   InputConstraints include/input_constraints.h:12-26
+ *   cmpc_set_reference     MpcQpSolver::SetOutputReference include/mpc_qp_solver.h:94,
+ *                          NerveCenter::SetOutputReference include/nerve_center.h:119-122
+ *   cmpc_set_state         DistributedController::Initialize (u_old_) libs/distributed_controller.cc:27-67,
+ *                          NerveCenter du_old_ include/nerve_center.h:73,94
+ *   cmpc_upload_lin        AugmentedLinearizedSystem::Update result (A,B,C,f)
+ *                          libs/aug_lin_sys.cc:145-177 + Observer state estimate
+ *   cmpc_build             GenerateInitialQP libs/distributed_controller.cc:72-108 =
+ *                          AdjustAllDelayedStates include/aug_lin_sys.h:141-154
+ *                          + GeneratePrediction libs/aug_lin_sys.cc:260-334
+ *                          + GenerateDistributedQP include/distributed_solver.h:83-94
+ *                          + GenerateQP libs/mpc_qp_solver.cc:16-40
+ *   cmpc_init_warmstart    MpcQpSolver::InitializeQPProblem libs/mpc_qp_solver.cc:77-101
+ *   cmpc_iterate           Jacobi loop include/nerve_center.h:146-172 (SolveQPHelper :276-296,
+ *                          DistributedController::GetInput include/distributed_controller.h:206-226,
+ *                          ApplyOtherInput include/distributed_solver.h:98-103,
+ *                          SolveQP libs/mpc_qp_solver.cc:42-75, UpdateUOld/SendUHelper
+ *                          include/nerve_center.h:313-328)
+ *   cmpc_step              cmpc_build + cmpc_iterate = NerveCenter::GetNextInputWithTiming
+ *                          include/nerve_center.h:134-182
+ *
+ * The QP solver is this library's own warm-started dual active-set method
+ * (qpOASES 3.2.0 SQProblem::hotstart is not vendored in the reference); it
+ * keeps the reference's n_wsr_max = 10 cap (include/mpc_qp_solver.h:24) and
+ * the zero-move fallback on any non-success (libs/mpc_qp_solver.cc:66-69).
+ */
+#ifndef CMPC_H
+#define CMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPC_MAX_INPUTS 8   /* nu_tot */
+#define CMPC_MAX_NV 8       /* m * nu */
+#define CMPC_MAX_NS 15      /* plant states (+ inputs <= 16 lanes) */
+#define CMPC_NWSR_MAX 10    /* include/mpc_qp_solver.h:24 */
+
+/* QP status words (per QP slot, last solve of the step) */
+#define CMPC_QP_OK 0          /* qpOASES::SUCCESSFUL_RETURN */
+#define CMPC_QP_MAX_NWSR 1    /* > n_wsr_max working-set changes -> zero move */
+#define CMPC_QP_INFEASIBLE 2  /* -> zero move */
+#define CMPC_QP_NOT_PD 3      /* Hessian not positive definite -> zero move */
+
+/* cmpc_iterate / cmpc_step flags */
+#define CMPC_APPLY_MOVE 1u    /* u_old += first move (UpdateUOld/SendUHelper) */
+#define CMPC_TRACE 2u         /* record working-set change sequences */
+
+/* Problem dimensions.  All sub-controllers of a context share them
+ * (coop: every sub-controller has nu own inputs, nu_tot - nu other inputs). */
+typedef struct cmpc_dims {
+  int32_t ns;      /* plant states                   AugmentedLinearizedSystem::n_states */
+  int32_t ndist;   /* disturbance/integrator states  n_disturbance_states */
+  int32_t nu_tot;  /* plant control inputs           n_control_inputs */
+  int32_t nu;      /* own inputs per sub-controller  n_sub_control_inputs */
+  int32_t ny;      /* controlled outputs             ControlledOutputIndices::size */
+  int32_t p;       /* prediction horizon */
+  int32_t m;       /* move horizon */
+  int32_t delay[CMPC_MAX_INPUTS]; /* Delays, per sub-controller-ordered input */
+  int32_t S;       /* sub-controllers per scenario (NerveCenter pack size) */
+  int32_t B;       /* independent scenarios in the batch */
+} cmpc_dims;
+
+/* Derived sizes and the packed per-QP input record ("lin record").
+ * One record per QP slot q = b * S + s (scenario-major), doubles, row-major:
+ *   [off_A ] Aorig   ns x ns        discrete A       (AComposite::Aorig)
+ *   [off_B ] Bin     ns x nu_tot    column c = input c of this sub-controller's
+ *                                   ordering: Borig column if delay[c]==0,
+ *                                   Adelay column otherwise (BComposite/AComposite)
+ *   [off_C ] Csel    ny x nobs      controlled rows of C = [Cplant | I_dist]
+ *   [off_f ] fd      ns             discrete affine term (GetDerivative())
+ *   [off_x ] dxaug   naug           observer augmented state tail: ndist
+ *                                   disturbance, nd delayed-input slots, then
+ *                                   per delayed input delay-1 shift states
+ *                                   (raw: AdjustAllDelayedStates is applied here)
+ *   [off_y ] yprev   ny             controlled part of the measured output
+ * stride = rec_len (multiple of 8 doubles). */
+typedef struct cmpc_layout {
+  int32_t nd, n_delay_states, naug, nobs, ntot, nV, nuo, nVo;
+  int32_t off_A, off_B, off_C, off_f, off_x, off_y, rec_len;
+} cmpc_layout;
+
+/* Fill *L from *d.  Returns 0, or <0 if the dimensions are unsupported. */
+int cmpc_layout_of(const cmpc_dims* d, cmpc_layout* L);
+
+typedef struct cmpc_ctx cmpc_ctx;
+
+/* Context on HIP device `device`, all work on a private non-blocking stream
+ * unless cmpc_set_stream() is called. */
+int cmpc_create(cmpc_ctx** ctx, const cmpc_dims* dims, int device);
+int cmpc_destroy(cmpc_ctx* ctx);
+int cmpc_set_stream(cmpc_ctx* ctx, void* hip_stream);
+const char* cmpc_last_error(void);
+int cmpc_get_layout(const cmpc_ctx* ctx, cmpc_layout* L);
+
+/* Per sub-controller configuration (s = 0..S-1), shared by all scenarios. */
+int cmpc_set_weights(cmpc_ctx* ctx, int s, const double* uwt /* nu x nu */,
+                     const double* ywt /* ny x ny */);
+int cmpc_set_constraints(cmpc_ctx* ctx, int s, const double* lower,
+                         const double* upper, const double* rate_lower,
+                         const double* rate_upper); /* each nu */
+int cmpc_set_reference(cmpc_ctx* ctx, int s, const double* y_ref /* p x ny */);
+
+/* Mutable per-slot state.  Any pointer may be NULL (left unchanged).
+ * u_old  : B*S*nu_tot  sub-controller's u_old_ in its own input ordering
+ * du_old : B*S*nV      previous step's move plans (NerveCenter::du_old_)
+ * ws     : B*S         warm-start working-set words */
+int cmpc_set_state(cmpc_ctx* ctx, const double* u_old, const double* du_old,
+                   const uint32_t* ws);
+int cmpc_get_state(cmpc_ctx* ctx, double* u_old, double* du_old, uint32_t* ws);
+
+/* Inputs: B*S lin records from host memory (H2D copy on the ctx stream), or
+ * written in place by a device-side producer through cmpc_lin_device(). */
+int cmpc_upload_lin(cmpc_ctx* ctx, const double* lin_host);
+void* cmpc_lin_device(cmpc_ctx* ctx);
+
+/* Hot path. */
+int cmpc_build(cmpc_ctx* ctx);
+int cmpc_init_warmstart(cmpc_ctx* ctx);
+int cmpc_iterate(cmpc_ctx* ctx, int K, uint32_t flags);
+int cmpc_step(cmpc_ctx* ctx, int K, uint32_t flags);
+int cmpc_synchronize(cmpc_ctx* ctx);
+
+/* Results of the last cmpc_iterate (any pointer may be NULL).
+ * du: B*S*nV move plans; status/nwsr: B*S of the last solve. */
+int cmpc_download(cmpc_ctx* ctx, double* du, int32_t* status, int32_t* nwsr);
+/* The condensed QPs of the last cmpc_build (parity/debug):
+ * H: B*S*nV*nV (row-major), f: B*S*nV, G: B*S*nV*nVo (G = Su' W Su_other). */
+int cmpc_download_qp(cmpc_ctx* ctx, double* H, double* f, double* G);
+/* Working-set change sequences of the last traced cmpc_iterate:
+ * trace: B*S*K*16 bytes (bit7 add, bit6 upper side, bits0-5 constraint j;
+ * 0xFF terminates), ntrace: B*S*K counts. */
+int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
+
+/* Per-kernel device time (HIP events on the ctx stream, opt-in). */
+#define CMPC_KERNEL_BUILD 0
+#define CMPC_KERNEL_ITERATE 1
+int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
+int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,
+                     int64_t* launches);
+
+/* Upstream producer (host, untimed): AugmentedLinearizedSystem::Update for the
+ * reference plants — linearise the plant at (x, u_full), discretise
+ * (Taylor-4, libs/aug_lin_sys.cc:232-255), reorder the inputs by input_order
+ * (ControlInputIndices) and fill off_A..off_f of one lin record for the
+ * controlled outputs out_idx[0..ny-1].  plant: 0 parallel, 1 serial. */
+#define CMPC_PLANT_PARALLEL 0
+#define CMPC_PLANT_SERIAL 1
+int cmpc_plant_dims(int plant, int* ns, int* n_inputs, int* n_outputs,
+                    int* n_control_inputs);
+int cmpc_plant_default(int plant, double* x, double* u_full);
+int cmpc_plant_output(int plant, const double* x, double* y);
+int cmpc_plant_lin_record(int plant, double p_in, double p_out, double Ts,
+                          const double* x, const double* u_full,
+                          const int32_t* input_order, const int32_t* out_idx,
+                          const cmpc_dims* dims, double* record);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMPC_H */

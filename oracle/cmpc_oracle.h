@@ -1,0 +1,118 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * CPU restatement of the reference's condensed-QP hot path
+ * (katie-jones/compressor-mpc):
+ *   or_plant.c     plant linearisation + Taylor-4 discretisation (upstream
+ *                  producer, needed to pin against the step-0 golden records)
+ *   or_condense.c  AugmentedLinearizedSystem (Update reorder, AComposite,
+ *                  BComposite, GeneratePrediction, AdjustAllDelayedStates),
+ *                  MpcQpSolver::SetWeights/GenerateQP/SolveQP bounds,
+ *                  DistributedSolver::GenerateDistributedQP/ApplyOtherInput,
+ *                  in the reference's own operation order (O(p^2) Su loop,
+ *                  dense products)
+ *   or_qp.c        the build's warm-started dual active-set QP solver
+ *                  (replaces qpOASES 3.2.0 SQProblem::hotstart, which is not
+ *                  vendored in the reference; parity of the QP arithmetic to
+ *                  qpOASES itself is pinned only through the unique optimum
+ *                  and the six step-0 golden records)
+ *   or_nerve.c     NerveCenter Jacobi loop / DistributedController::GetInput
+ *                  over a batch in the product's lin-record format
+ *
+ * The product must never route through this library.
+ */
+#ifndef CMPC_ORACLE_H
+#define CMPC_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/cmpc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_PLANT_PARALLEL 0
+#define OR_PLANT_SERIAL 1
+
+/* ---- plant (or_plant.c) ---- */
+int or_plant_dims(int plant, int* ns, int* ni, int* no, int* nci);
+void or_plant_default(int plant, double* x, double* u);
+void or_plant_linearize(int plant, double p_in, double p_out, const double* x,
+                        const double* u, double* A, double* B, double* C,
+                        double* f);
+void or_plant_output(int plant, const double* x, double* y);
+void or_discretize_rk4(int ns, int nci, double Ts, const double* A,
+                       const double* B, const double* f, double* Ad,
+                       double* Bd, double* fd);
+
+/* ---- layout (restates cmpc.h's documented record format) ---- */
+int or_layout_of(const cmpc_dims* d, cmpc_layout* L);
+
+/* AugmentedLinearizedSystem::Update (libs/aug_lin_sys.cc:145-177) +
+ * controlled-row selection of C: fills off_A..off_f of a lin record. */
+int or_lin_record(int plant, double p_in, double p_out, double Ts,
+                  const double* x, const double* u_full,
+                  const int32_t* input_order, const int32_t* out_idx,
+                  const cmpc_dims* d, double* rec);
+
+/* ---- condensation (or_condense.c) ---- */
+/* GeneratePrediction (libs/aug_lin_sys.cc:260-334).  Row-major outputs:
+ * Su (p*ny) x (m*nu), Sx (p*ny) x naug, Sf (p*ny) x ns,
+ * Su_other (p*ny) x (m*nuo) (may be NULL when nuo == 0). */
+int or_generate_prediction(const cmpc_dims* d, const double* rec, double* Su,
+                           double* Sx, double* Sf, double* Su_other);
+
+/* Full sub-controller build = GenerateInitialQP: delta_x0 assembly
+ * (libs/distributed_controller.cc:85-90), AdjustAllDelayedStates,
+ * GeneratePrediction, GenerateDistributedQP (YPW = W*Su) and GenerateQP.
+ * Outputs H (nV x nV, row-major, not symmetrised — as the reference),
+ * f (nV), YPW ((p*ny) x nV), Su_other ((p*ny) x nVo), G = Su'W Su_other
+ * (nV x nVo, for cross-checks only; the oracle's iterate uses YPW/Su_other). */
+int or_build_qp(const cmpc_dims* d, const double* rec, const double* u_old,
+                const double* y_ref, const double* ywt, const double* uwt,
+                double* H, double* f, double* YPW, double* Su_other,
+                double* G);
+
+/* ---- QP (or_qp.c) ---- */
+typedef struct or_qp_info {
+  int32_t status;  /* CMPC_QP_* */
+  int32_t nchg;    /* working-set changes used */
+  uint32_t ws;     /* working set on exit */
+  int32_t ntrace;
+  uint8_t trace[16];
+} or_qp_info;
+
+/* min 1/2 x'Hx + g'x  s.t. lb <= x <= ub, lbA <= A x <= ubA with the
+ * reference's rate-constraint matrix A (include/mpc_qp_solver.h:108-123). */
+int or_qp_solve(int n, int nu, const double* H, const double* g,
+                const double* lb, const double* ub, const double* lbA,
+                const double* ubA, uint32_t ws_in, int max_chg, double* x,
+                or_qp_info* info);
+
+/* ---- batched NerveCenter step (or_nerve.c) ---- */
+typedef struct or_cfg {
+  const double* y_ref; /* S x (p*ny) */
+  const double* ywt;   /* S x (ny*ny) */
+  const double* uwt;   /* S x (nu*nu) */
+  const double* lower; /* S x nu each */
+  const double* upper;
+  const double* rate_lower;
+  const double* rate_upper;
+} or_cfg;
+
+/* One control step for all B scenarios (build + K Jacobi iterations), on
+ * `threads` OpenMP threads (1 = the reference's execution model).
+ * State in/out: u_old (B*S*nu_tot), du_old (B*S*nV), ws (B*S).
+ * Outputs: du (B*S*nV), status/nwsr (B*S), optional trace (B*S*K*16 bytes)
+ * and ntrace (B*S*K). init != 0 first runs InitializeQPProblem (cold solve,
+ * status ignored) on each QP.  Returns 0. */
+int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
+            uint32_t flags, int init, int threads, double* u_old,
+            double* du_old, uint32_t* ws, double* du, int32_t* status,
+            int32_t* nwsr, uint8_t* trace, int32_t* ntrace);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
