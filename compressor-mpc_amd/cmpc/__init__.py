@@ -1,0 +1,207 @@
+"""cmpc — MI355X-native condensed-QP hot path of katie-jones/compressor-mpc.
+
+Python host view of the C ABI (include/cmpc.h).  Every compute call goes to
+libcmpc.so (HIP kernels for gfx950); there is no CPU fallback.
+
+    ctx = Context(cfg, B)                 # NerveCenter/DistributedController ctors
+    ctx.configure(arrays)                 # SetWeights / SetOutputReference / constraints
+    ctx.set_state(u_old, du_old, ws)      # Initialize
+    ctx.upload_lin(lin)                   # AugmentedLinearizedSystem::Update results
+    ctx.init_warmstart()                  # InitializeQPProblem
+    ctx.step(K)                           # GetNextInputWithTiming (build + K Jacobi iterations)
+    du, status, nwsr = ctx.download()
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import (CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE, CMPC_QP_INFEASIBLE,
+                   CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
+                   CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
+from .configs import ControllerConfig, SetupFile, reference_config
+from .problem import ControllerArrays, controller_arrays, plant_input_from_plans
+
+__all__ = ["Context", "ControllerConfig", "SetupFile", "reference_config", "controller_arrays",
+           "plant_input_from_plans", "plant_lin_record", "plant_default", "plant_output",
+           "layout_of", "qp_solve_batch", "CMPC_APPLY_MOVE", "CMPC_TRACE", "CMPC_QP_OK",
+           "CMPC_QP_MAX_NWSR", "CMPC_QP_INFEASIBLE", "CMPC_QP_NOT_PD"]
+
+
+def layout_of(dims: CmpcDims) -> CmpcLayout:
+    L = CmpcLayout()
+    check(load_library().cmpc_layout_of(ctypes.byref(dims), ctypes.byref(L)), "cmpc_layout_of")
+    return L
+
+
+def plant_default(plant: int):
+    x = np.zeros(16)
+    u = np.zeros(16)
+    check(load_library().cmpc_plant_default(plant, dptr(x), dptr(u)), "cmpc_plant_default")
+    ns, ni = (11, 9) if plant == 0 else (10, 8)
+    return x[:ns].copy(), u[:ni].copy()
+
+
+def plant_output(plant: int, x) -> np.ndarray:
+    y = np.zeros(4)
+    check(load_library().cmpc_plant_output(plant, dptr(np.ascontiguousarray(x, np.float64)),
+                                            dptr(y)), "cmpc_plant_output")
+    return y
+
+
+def plant_lin_record(cfg: ControllerConfig, dims: CmpcDims, s: int, x, u_full, Ts=0.05,
+                     p_in=1.0, p_out=1.0, out=None) -> np.ndarray:
+    """AugmentedLinearizedSystem::Update for sub-controller s -> lin record
+    (fills Aorig, Bin, Csel, fd; dx_aug and yprev are left as they are)."""
+    L = layout_of(dims)
+    rec = np.zeros(L.rec_len) if out is None else out
+    io = np.ascontiguousarray(cfg.input_order[s], dtype=np.int32)
+    oi = np.ascontiguousarray(cfg.out_idx[s], dtype=np.int32)
+    check(load_library().cmpc_plant_lin_record(
+        cfg.plant, p_in, p_out, Ts, dptr(np.ascontiguousarray(x, np.float64)),
+        dptr(np.ascontiguousarray(u_full, np.float64)), iptr(io), iptr(oi), ctypes.byref(dims),
+        dptr(rec)), "cmpc_plant_lin_record")
+    return rec
+
+
+def qp_solve_batch(H, g, lb, ub, lbA, ubA, nu, ws_in=None, max_chg=10, device=0):
+    """The device QP solver alone over a batch (parity / known-answer tests)."""
+    H = np.ascontiguousarray(H, np.float64)
+    nqp, n = g.shape
+    c = lambda a: np.ascontiguousarray(a, np.float64)
+    ws_in = np.zeros(nqp, np.uint32) if ws_in is None else np.ascontiguousarray(ws_in, np.uint32)
+    x = np.zeros((nqp, n))
+    status = np.zeros(nqp, np.int32)
+    nchg = np.zeros(nqp, np.int32)
+    ws_out = np.zeros(nqp, np.uint32)
+    trace = np.zeros((nqp, 16), np.uint8)
+    ntrace = np.zeros(nqp, np.int32)
+    lib = load_library()
+    lib.cmpc_qp_solve_batch.restype = ctypes.c_int
+    check(lib.cmpc_qp_solve_batch(device, n, nu, nqp, dptr(H), dptr(c(g)), dptr(c(lb)),
+                                  dptr(c(ub)), dptr(c(lbA)), dptr(c(ubA)), uptr(ws_in), max_chg,
+                                  dptr(x), iptr(status), iptr(nchg), uptr(ws_out), bptr(trace),
+                                  iptr(ntrace)), "cmpc_qp_solve_batch")
+    return x, status, nchg, ws_out, trace, ntrace
+
+
+class Context:
+    """One batched NerveCenter over B scenarios of cfg.S sub-controllers."""
+
+    def __init__(self, cfg: ControllerConfig, B: int, device: int = 0):
+        self.lib = load_library()
+        self.cfg = cfg
+        self.B = B
+        self.dims = CmpcDims.from_config(cfg, B)
+        self.layout = layout_of(self.dims)
+        self.nqp = B * cfg.S
+        self._h = ctypes.c_void_p()
+        check(self.lib.cmpc_create(ctypes.byref(self._h), ctypes.byref(self.dims), device),
+              "cmpc_create")
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if self._h:
+            self.lib.cmpc_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int):
+        check(self.lib.cmpc_set_stream(self._h, ctypes.c_void_p(stream_handle)), "cmpc_set_stream")
+
+    # -- configuration ---------------------------------------------------
+    def configure(self, a: ControllerArrays):
+        for s in range(self.cfg.S):
+            check(self.lib.cmpc_set_weights(self._h, s, dptr(np.ascontiguousarray(a.uwt[s])),
+                                            dptr(np.ascontiguousarray(a.ywt[s]))), "set_weights")
+            check(self.lib.cmpc_set_constraints(
+                self._h, s, dptr(np.ascontiguousarray(a.lower[s])),
+                dptr(np.ascontiguousarray(a.upper[s])), dptr(np.ascontiguousarray(a.rate_lower[s])),
+                dptr(np.ascontiguousarray(a.rate_upper[s]))), "set_constraints")
+            check(self.lib.cmpc_set_reference(self._h, s, dptr(np.ascontiguousarray(a.y_ref[s]))),
+                  "set_reference")
+
+    def set_state(self, u_old=None, du_old=None, ws=None):
+        c = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)
+        u_old, du_old, ws = c(u_old, np.float64), c(du_old, np.float64), c(ws, np.uint32)
+        check(self.lib.cmpc_set_state(self._h, dptr(u_old) if u_old is not None else None,
+                                      dptr(du_old) if du_old is not None else None,
+                                      uptr(ws) if ws is not None else None), "set_state")
+
+    def get_state(self):
+        u_old = np.zeros((self.nqp, self.cfg.nu_tot))
+        du_old = np.zeros((self.nqp, self.layout.nV))
+        ws = np.zeros(self.nqp, np.uint32)
+        check(self.lib.cmpc_get_state(self._h, dptr(u_old), dptr(du_old), uptr(ws)), "get_state")
+        return u_old, du_old, ws
+
+    def upload_lin(self, lin: np.ndarray):
+        lin = np.ascontiguousarray(lin, np.float64)
+        assert lin.size == self.nqp * self.layout.rec_len
+        check(self.lib.cmpc_upload_lin(self._h, dptr(lin)), "upload_lin")
+
+    def lin_device_ptr(self) -> int:
+        return self.lib.cmpc_lin_device(self._h)
+
+    def bind_lin(self, device_ptr: int = 0):
+        """Bind an external device-resident record array (0 = own buffer)."""
+        check(self.lib.cmpc_bind_lin(self._h, ctypes.c_void_p(device_ptr or None)), "cmpc_bind_lin")
+
+    # -- hot path --------------------------------------------------------
+    def build(self):
+        check(self.lib.cmpc_build(self._h), "cmpc_build")
+
+    def init_warmstart(self):
+        check(self.lib.cmpc_init_warmstart(self._h), "cmpc_init_warmstart")
+
+    def iterate(self, K: int, flags: int = 0):
+        check(self.lib.cmpc_iterate(self._h, K, flags), "cmpc_iterate")
+
+    def step(self, K: int, flags: int = 0):
+        check(self.lib.cmpc_step(self._h, K, flags), "cmpc_step")
+
+    def synchronize(self):
+        check(self.lib.cmpc_synchronize(self._h), "cmpc_synchronize")
+
+    # -- results ---------------------------------------------------------
+    def download(self):
+        du = np.zeros((self.nqp, self.layout.nV))
+        status = np.zeros(self.nqp, np.int32)
+        nwsr = np.zeros(self.nqp, np.int32)
+        check(self.lib.cmpc_download(self._h, dptr(du), iptr(status), iptr(nwsr)), "download")
+        return du, status, nwsr
+
+    def download_qp(self):
+        nV, nVo = self.layout.nV, self.layout.nVo
+        H = np.zeros((self.nqp, nV, nV))
+        f = np.zeros((self.nqp, nV))
+        G = np.zeros((self.nqp, nV, max(nVo, 1)))
+        check(self.lib.cmpc_download_qp(self._h, dptr(H), dptr(f), dptr(G)), "download_qp")
+        return H, f, G[:, :, :nVo]
+
+    def download_trace(self, K: int):
+        trace = np.zeros((self.nqp, K, 16), np.uint8)
+        ntrace = np.zeros((self.nqp, K), np.int32)
+        check(self.lib.cmpc_download_trace(self._h, bptr(trace), iptr(ntrace)), "download_trace")
+        return trace, ntrace
+
+    def enable_timing(self, on: bool = True):
+        check(self.lib.cmpc_enable_timing(self._h, int(on)), "enable_timing")
+
+    def kernel_time(self, kernel: int):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self.lib.cmpc_kernel_time(self._h, kernel, ctypes.byref(ms), ctypes.byref(n)),
+              "kernel_time")
+        return ms.value, n.value

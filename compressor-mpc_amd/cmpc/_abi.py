@@ -80,7 +80,7 @@ EXPORTS = (
     "cmpc_lin_device", "cmpc_build", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
-    "cmpc_plant_output", "cmpc_plant_lin_record",
+    "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
 )
 
 _lib = None
@@ -114,6 +114,7 @@ def load_library(path: str = LIB_PATH):
         "cmpc_get_state": ([c_void, P(dbl), P(dbl), P(u32)], ctypes.c_int),
         "cmpc_upload_lin": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_lin_device": ([c_void], c_void),
+        "cmpc_bind_lin": ([c_void, c_void], ctypes.c_int),
         "cmpc_build": ([c_void], ctypes.c_int),
         "cmpc_init_warmstart": ([c_void], ctypes.c_int),
         "cmpc_iterate": ([c_void, ctypes.c_int, u32], ctypes.c_int),
@@ -130,6 +131,10 @@ def load_library(path: str = LIB_PATH):
         "cmpc_plant_output": ([ctypes.c_int, P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_plant_lin_record": ([ctypes.c_int, dbl, dbl, dbl, P(dbl), P(dbl), P(i32), P(i32),
                                    P(CmpcDims), P(dbl)], ctypes.c_int),
+        "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),
+                                 P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32), ctypes.c_int,
+                                 P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],
+                                ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

@@ -1,0 +1,67 @@
+"""Seeded synthetic batches of the reference workload.
+
+Per scenario b (seed = 1000 + config_id unless given):
+  x_b = x_def * (1 + 0.01 N(0,1))          x_def: include/parallel_compressors.h:74-78
+  u_b = u_def + U(-0.02, 0.02) on the control entries  (:81-86)
+  linearise + discretise at (x_b, u_b), Ts = 0.05, on the host (untimed);
+  an operating point whose discrete A has spectral radius > 1 is redrawn
+  (about 9% of parallel-plant draws: a 1% pressure perturbation can bring a
+  compressor's discharge pressure to the tank pressure, where the valve
+  derivative ~ 1/sqrt|dp| explodes; the nominal radius is 0.995)
+Per QP slot (scenario b, sub-controller s):
+  dx_aug tail ~ N(0, 1e-3)
+  u_old: torque inputs ~ U(-0.05, 0.05), recycle inputs ~ U(0, 0.05)
+  y_prev = plant output at x_b (controlled entries)
+  du_old = 0, ws = 0
+"""
+import numpy as np
+
+from ._abi import CmpcDims
+from .configs import REF_TS, ControllerConfig
+from . import plant_default, plant_lin_record, plant_output, layout_of
+
+CONTROL_ENTRIES = (0, 3, 4, 7)   # ControlInputIndex <0,3,4,7> of both plants
+
+
+def synthetic_batch(cfg: ControllerConfig, B: int, seed: int = 1002, n_distinct: int = None):
+    """Returns (lin [B*S, rec_len], u_old [B*S, nu_tot], du_old, ws).
+
+    n_distinct: number of distinct linearisations to compute (the rest of the
+    batch cycles through them with fresh dx_aug / u_old draws) — the host-side
+    producer is not what is measured, this only bounds set-up time."""
+    rng = np.random.default_rng(seed)
+    dims = CmpcDims.from_config(cfg, B)
+    L = layout_of(dims)
+    S = cfg.S
+    nq = B * S
+    nd = n_distinct or B
+    x_def, u_def = plant_default(cfg.plant)
+    base = np.zeros((nd, S, L.rec_len))
+    ys = np.zeros((nd, 4))
+    ns = cfg.ns
+    for i in range(nd):
+        while True:
+            x = x_def * (1.0 + 0.01 * rng.standard_normal(x_def.shape))
+            u = u_def.copy()
+            u[list(CONTROL_ENTRIES)] += rng.uniform(-0.02, 0.02, len(CONTROL_ENTRIES))
+            for s in range(S):
+                plant_lin_record(cfg, dims, s, x, u, Ts=REF_TS, out=base[i, s])
+            A = base[i, 0, L.off_A:L.off_A + ns * ns].reshape(ns, ns)
+            if np.all(np.isfinite(base[i])) and np.abs(np.linalg.eigvals(A)).max() <= 1.0:
+                break
+        ys[i] = plant_output(cfg.plant, x)
+    lin = np.ascontiguousarray(np.tile(base, ((B + nd - 1) // nd, 1, 1))[:B])
+    idx = np.arange(B) % nd
+    for s in range(S):
+        lin[:, s, L.off_x:L.off_x + L.naug] = 1e-3 * rng.standard_normal((B, L.naug))
+        lin[:, s, L.off_y:L.off_y + cfg.ny] = ys[idx][:, cfg.out_idx[s]]
+    lin = lin.reshape(nq, L.rec_len)
+    u_old = np.zeros((B, S, cfg.nu_tot))
+    for s in range(S):
+        for c, plant_c in enumerate(cfg.input_order[s]):
+            torque = plant_c in (0, 2)     # control inputs: torque1, rec1, torque2, rec2
+            u_old[:, s, c] = (rng.uniform(-0.05, 0.05, B) if torque else rng.uniform(0.0, 0.05, B))
+    u_old = np.ascontiguousarray(u_old.reshape(nq, cfg.nu_tot))
+    du_old = np.zeros((nq, cfg.nV))
+    ws = np.zeros(nq, np.uint32)
+    return np.ascontiguousarray(lin), u_old, du_old, ws

@@ -1,0 +1,630 @@
+// Host implementation of the C ABI declared in include/cmpc.h.
+//
+// The context owns every batched device buffer (HBM-resident between steps):
+//   lin    B*S lin records (inputs of the build kernel)
+//   qp     B*S condensed QPs [H | f | G]      (build -> iterate hand-off)
+//   cfg    S per-sub-controller blocks          (weights, reference, bounds)
+//   state  u_old, du_old, ws                   (persist across steps, as the
+//                                               reference's member state)
+//   out    du, status, nwsr, trace
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cmpc_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+int layout_of(const cmpc_dims* d, cmpc_layout* L) {
+  if (!d || !L) return fail("null argument");
+  if (d->ns < 1 || d->ns > CMPC_MAX_NS || d->nu_tot < 1 || d->nu_tot > CMPC_MAX_INPUTS ||
+      d->nu < 1 || d->nu > d->nu_tot || d->ny < 1 || d->p < 1 || d->m < 1 || d->m > d->p ||
+      d->m * d->nu > CMPC_MAX_NV || d->ndist < 0 || d->S < 1 || d->B < 1)
+    return fail("invalid dimensions");
+  std::memset(L, 0, sizeof *L);
+  for (int i = 0; i < d->nu_tot; ++i) {
+    if (d->delay[i] < 0) return fail("negative delay");
+    if (d->delay[i]) L->nd++;
+    L->n_delay_states += d->delay[i];
+  }
+  L->naug = d->ndist + L->n_delay_states;
+  L->nobs = d->ns + d->ndist;
+  L->ntot = L->nobs + L->n_delay_states;
+  L->nV = d->m * d->nu;
+  L->nuo = d->nu_tot - d->nu;
+  L->nVo = d->m * L->nuo;
+  L->off_A = 0;
+  L->off_B = d->ns * d->ns;
+  L->off_C = L->off_B + d->ns * d->nu_tot;
+  L->off_f = L->off_C + d->ny * L->nobs;
+  L->off_x = L->off_f + d->ns;
+  L->off_y = L->off_x + L->naug;
+  L->rec_len = ((L->off_y + d->ny) + 7) / 8 * 8;
+  return 0;
+}
+
+}  // namespace
+
+struct cmpc_ctx {
+  cmpc_dims d{};
+  cmpc_layout L{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int nqp = 0, qp_len = 0;
+  CfgOffsets co{};
+  // host mirror of the configuration
+  std::vector<double> ywt, uwt, yref, lower, upper, rlower, rupper;  // per s
+  std::vector<double> h_cfg;
+  std::vector<int> have_w, have_c, have_r;
+  bool cfg_dirty = true;
+  // device buffers
+  const double* lin_bound = nullptr;  // external records (cmpc_bind_lin)
+  double *lin = nullptr, *qp = nullptr, *cfg = nullptr, *u_old = nullptr, *du_old = nullptr,
+         *du = nullptr;
+  uint32_t* ws = nullptr;
+  int32_t *status = nullptr, *nwsr = nullptr, *ntrace = nullptr;
+  uint8_t* trace = nullptr;
+  size_t trace_cap = 0;
+  int trace_K = 0;
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
+  double tot_ms[2] = {0, 0};
+  int64_t launches[2] = {0, 0};
+};
+
+namespace {
+
+int rebuild_cfg(cmpc_ctx* c) {
+  const cmpc_dims& d = c->d;
+  const int S = d.S, ny = d.ny, nu = d.nu, p = d.p;
+  for (int s = 0; s < S; ++s)
+    if (!c->have_w[s] || !c->have_c[s] || !c->have_r[s])
+      return fail("sub-controller " + std::to_string(s) +
+                  ": weights, constraints and reference must all be set before the step");
+  c->h_cfg.assign((size_t)S * c->co.len, 0.0);
+  for (int s = 0; s < S; ++s) {
+    double* b = c->h_cfg.data() + (size_t)s * c->co.len;
+    // ywt = L_W L_W' (Cholesky; zero pivots allowed for PSD weights)
+    const double* W = c->ywt.data() + (size_t)s * ny * ny;
+    std::vector<double> Lw(ny * ny, 0.0);
+    double scale = 0;
+    for (int i = 0; i < ny * ny; ++i) scale = std::max(scale, std::fabs(W[i]));
+    for (int i = 0; i < ny; ++i)
+      for (int j = 0; j < ny; ++j)
+        if (std::fabs(W[i * ny + j] - W[j * ny + i]) > 1e-12 * (1 + scale))
+          return fail("ywt must be symmetric");
+    for (int j = 0; j < ny; ++j) {
+      double dd = W[j * ny + j];
+      for (int k = 0; k < j; ++k) dd -= Lw[j * ny + k] * Lw[j * ny + k];
+      if (dd < -1e-12 * (1 + scale)) return fail("ywt must be positive semi-definite");
+      if (dd <= 1e-14 * (1 + scale)) continue;  // zero column
+      const double ljj = std::sqrt(dd);
+      Lw[j * ny + j] = ljj;
+      for (int i = j + 1; i < ny; ++i) {
+        double v = W[i * ny + j];
+        for (int k = 0; k < j; ++k) v -= Lw[i * ny + k] * Lw[j * ny + k];
+        Lw[i * ny + j] = v / ljj;
+      }
+    }
+    for (int o = 0; o < ny; ++o)  // lwt = L_W' (upper triangular)
+      for (int o2 = 0; o2 < ny; ++o2) b[c->co.lwt + o * ny + o2] = Lw[o2 * ny + o];
+    const double* yr = c->yref.data() + (size_t)s * p * ny;
+    for (int r = 0; r < p; ++r)
+      for (int o = 0; o < ny; ++o) {
+        double v = 0;
+        for (int o2 = o; o2 < ny; ++o2) v += Lw[o2 * ny + o] * yr[r * ny + o2];
+        b[c->co.yhat + r * ny + o] = v;
+      }
+    std::memcpy(b + c->co.uwt, c->uwt.data() + (size_t)s * nu * nu, sizeof(double) * nu * nu);
+    std::memcpy(b + c->co.lower, c->lower.data() + (size_t)s * nu, sizeof(double) * nu);
+    std::memcpy(b + c->co.upper, c->upper.data() + (size_t)s * nu, sizeof(double) * nu);
+    std::memcpy(b + c->co.rlower, c->rlower.data() + (size_t)s * nu, sizeof(double) * nu);
+    std::memcpy(b + c->co.rupper, c->rupper.data() + (size_t)s * nu, sizeof(double) * nu);
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(c->cfg, c->h_cfg.data(), sizeof(double) * c->h_cfg.size(),
+                         hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->cfg_dirty = false;
+  return 0;
+}
+
+int ensure_cfg(cmpc_ctx* c) { return c->cfg_dirty ? rebuild_cfg(c) : 0; }
+
+int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
+  if (!c->timing) return 0;
+  HIP_TRY(hipEventCreate(e0));
+  HIP_TRY(hipEventRecord(*e0, c->stream));
+  (void)k;
+  return 0;
+}
+
+int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
+  if (!c->timing) return 0;
+  hipEvent_t e1;
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e1, c->stream));
+  c->pending[k].push_back({e0, e1});
+  c->launches[k]++;
+  return 0;
+}
+
+int resolve_timing(cmpc_ctx* c) {
+  for (int k = 0; k < 2; ++k) {
+    for (auto& pr : c->pending[k]) {
+      HIP_TRY(hipEventSynchronize(pr.second));
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+      c->tot_ms[k] += ms;
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    c->pending[k].clear();
+  }
+  return 0;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(std::string(what) + ": " + hipGetErrorString(e));
+  return 0;
+}
+
+int solve_params(cmpc_ctx* c, SolveParams* P) {
+  std::memset(P, 0, sizeof *P);
+  P->qp = c->qp;
+  P->cfg = c->cfg;
+  P->u_old = c->u_old;
+  P->du_old = c->du_old;
+  P->ws = c->ws;
+  P->du = c->du;
+  P->status = c->status;
+  P->nwsr = c->nwsr;
+  P->nqp = c->nqp;
+  P->S = c->d.S;
+  P->nu_tot = c->d.nu_tot;
+  P->qp_len = c->qp_len;
+  P->co = c->co;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_layout_of(const cmpc_dims* d, cmpc_layout* L) { return layout_of(d, L); }
+
+const char* cmpc_last_error(void) { return g_err.c_str(); }
+
+int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
+  if (!out || !dims) return fail("null argument");
+  *out = nullptr;
+  cmpc_layout L;
+  if (layout_of(dims, &L)) return -1;
+  const cmpc_dims& d = *dims;
+  if (64 % d.S != 0) return fail("S must divide the wavefront size (64)");
+  if (L.nuo != (d.S - 1) * d.nu)
+    return fail("nu_tot must equal S * nu (each sub-controller owns nu inputs)");
+  if (L.nd > CMPC_ND_MAX) return fail("more than 4 delayed inputs");
+  if (d.ns + d.nu_tot > 15) return fail("ns + nu_tot must be <= 15 (16-lane DPP rows)");
+  if (d.ny > 3) return fail("ny > 3 is not instantiated in the build kernel");
+  const long long nqp = (long long)d.B * d.S;
+  if (nqp > (1LL << 30)) return fail("batch too large");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail("no such HIP device");
+  cmpc_ctx* c = new cmpc_ctx();
+  c->d = d;
+  c->L = L;
+  c->device = device;
+  c->nqp = (int)nqp;
+  c->qp_len = (L.nV * L.nV + L.nV + L.nV * L.nVo + 1) / 2 * 2;
+  int off = 0;
+  c->co.lwt = off; off += d.ny * d.ny;
+  c->co.yhat = off; off += d.p * d.ny;
+  c->co.uwt = off; off += d.nu * d.nu;
+  c->co.lower = off; off += d.nu;
+  c->co.upper = off; off += d.nu;
+  c->co.rlower = off; off += d.nu;
+  c->co.rupper = off; off += d.nu;
+  c->co.len = (off + 1) / 2 * 2;
+  const int S = d.S;
+  c->ywt.assign((size_t)S * d.ny * d.ny, 0);
+  c->uwt.assign((size_t)S * d.nu * d.nu, 0);
+  c->yref.assign((size_t)S * d.p * d.ny, 0);
+  c->lower.assign((size_t)S * d.nu, 0);
+  c->upper.assign((size_t)S * d.nu, 0);
+  c->rlower.assign((size_t)S * d.nu, 0);
+  c->rupper.assign((size_t)S * d.nu, 0);
+  c->have_w.assign(S, 0);
+  c->have_c.assign(S, 0);
+  c->have_r.assign(S, 0);
+  auto cleanup = [&](int rc) {
+    cmpc_destroy(c);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return cleanup(fail("hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail("hipStreamCreate failed"));
+  c->own_stream = true;
+  const size_t n = (size_t)c->nqp;
+  if (hipMalloc(&c->lin, sizeof(double) * n * L.rec_len) != hipSuccess ||
+      hipMalloc(&c->qp, sizeof(double) * n * c->qp_len) != hipSuccess ||
+      hipMalloc(&c->cfg, sizeof(double) * (size_t)S * c->co.len) != hipSuccess ||
+      hipMalloc(&c->u_old, sizeof(double) * n * d.nu_tot) != hipSuccess ||
+      hipMalloc(&c->du_old, sizeof(double) * n * L.nV) != hipSuccess ||
+      hipMalloc(&c->du, sizeof(double) * n * L.nV) != hipSuccess ||
+      hipMalloc(&c->ws, sizeof(uint32_t) * n) != hipSuccess ||
+      hipMalloc(&c->status, sizeof(int32_t) * n) != hipSuccess ||
+      hipMalloc(&c->nwsr, sizeof(int32_t) * n) != hipSuccess)
+    return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
+  if (hipMemsetAsync(c->lin, 0, sizeof(double) * n * L.rec_len, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->qp, 0, sizeof(double) * n * c->qp_len, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->u_old, 0, sizeof(double) * n * d.nu_tot, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->du_old, 0, sizeof(double) * n * L.nV, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->du, 0, sizeof(double) * n * L.nV, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->ws, 0, sizeof(uint32_t) * n, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->status, 0, sizeof(int32_t) * n, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->nwsr, 0, sizeof(int32_t) * n, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return cleanup(fail("device initialisation failed"));
+  *out = c;
+  return 0;
+}
+
+int cmpc_destroy(cmpc_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int k = 0; k < 2; ++k)
+    for (auto& pr : c->pending[k]) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
+                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int cmpc_set_stream(cmpc_ctx* c, void* stream) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  c->stream = (hipStream_t)stream;
+  c->own_stream = false;
+  return 0;
+}
+
+int cmpc_get_layout(const cmpc_ctx* c, cmpc_layout* L) {
+  if (!c || !L) return fail("null argument");
+  *L = c->L;
+  return 0;
+}
+
+int cmpc_set_weights(cmpc_ctx* c, int s, const double* uwt, const double* ywt) {
+  if (!c || !uwt || !ywt) return fail("null argument");
+  if (s < 0 || s >= c->d.S) return fail("sub-controller index out of range");
+  const int ny = c->d.ny, nu = c->d.nu;
+  std::memcpy(c->ywt.data() + (size_t)s * ny * ny, ywt, sizeof(double) * ny * ny);
+  std::memcpy(c->uwt.data() + (size_t)s * nu * nu, uwt, sizeof(double) * nu * nu);
+  c->have_w[s] = 1;
+  c->cfg_dirty = true;
+  return 0;
+}
+
+int cmpc_set_constraints(cmpc_ctx* c, int s, const double* lo, const double* up,
+                         const double* rlo, const double* rup) {
+  if (!c || !lo || !up || !rlo || !rup) return fail("null argument");
+  if (s < 0 || s >= c->d.S) return fail("sub-controller index out of range");
+  const int nu = c->d.nu;
+  for (int i = 0; i < nu; ++i)
+    if (!(lo[i] <= up[i]) || !(rlo[i] <= rup[i]))
+      return fail("constraints must satisfy lower <= upper (NaN bounds are unset)");
+  std::memcpy(c->lower.data() + (size_t)s * nu, lo, sizeof(double) * nu);
+  std::memcpy(c->upper.data() + (size_t)s * nu, up, sizeof(double) * nu);
+  std::memcpy(c->rlower.data() + (size_t)s * nu, rlo, sizeof(double) * nu);
+  std::memcpy(c->rupper.data() + (size_t)s * nu, rup, sizeof(double) * nu);
+  c->have_c[s] = 1;
+  c->cfg_dirty = true;
+  return 0;
+}
+
+int cmpc_set_reference(cmpc_ctx* c, int s, const double* y_ref) {
+  if (!c || !y_ref) return fail("null argument");
+  if (s < 0 || s >= c->d.S) return fail("sub-controller index out of range");
+  const size_t n = (size_t)c->d.p * c->d.ny;
+  std::memcpy(c->yref.data() + s * n, y_ref, sizeof(double) * n);
+  c->have_r[s] = 1;
+  c->cfg_dirty = true;
+  return 0;
+}
+
+int cmpc_set_state(cmpc_ctx* c, const double* u_old, const double* du_old, const uint32_t* ws) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->nqp;
+  if (u_old)
+    HIP_TRY(hipMemcpyAsync(c->u_old, u_old, sizeof(double) * n * c->d.nu_tot,
+                           hipMemcpyHostToDevice, c->stream));
+  if (du_old)
+    HIP_TRY(hipMemcpyAsync(c->du_old, du_old, sizeof(double) * n * c->L.nV,
+                           hipMemcpyHostToDevice, c->stream));
+  if (ws) HIP_TRY(hipMemcpyAsync(c->ws, ws, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_get_state(cmpc_ctx* c, double* u_old, double* du_old, uint32_t* ws) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->nqp;
+  if (u_old)
+    HIP_TRY(hipMemcpyAsync(u_old, c->u_old, sizeof(double) * n * c->d.nu_tot,
+                           hipMemcpyDeviceToHost, c->stream));
+  if (du_old)
+    HIP_TRY(hipMemcpyAsync(du_old, c->du_old, sizeof(double) * n * c->L.nV,
+                           hipMemcpyDeviceToHost, c->stream));
+  if (ws) HIP_TRY(hipMemcpyAsync(ws, c->ws, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_upload_lin(cmpc_ctx* c, const double* lin) {
+  if (!c || !lin) return fail("null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(c->lin, lin, sizeof(double) * (size_t)c->nqp * c->L.rec_len,
+                         hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+void* cmpc_lin_device(cmpc_ctx* c) { return c ? (void*)c->lin : nullptr; }
+
+int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
+  if (!c) return fail("null context");
+  if (lin_device) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, lin_device) != hipSuccess || a.type != hipMemoryTypeDevice ||
+        a.device != c->device)
+      return fail("cmpc_bind_lin: not a device pointer on the context's device");
+  }
+  c->lin_bound = lin_device;
+  return 0;
+}
+
+int cmpc_build(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  if (ensure_cfg(c)) return -1;
+  HIP_TRY(hipSetDevice(c->device));
+  const cmpc_dims& d = c->d;
+  const cmpc_layout& L = c->L;
+  BuildParams P;
+  std::memset(&P, 0, sizeof P);
+  P.lin = c->lin_bound ? c->lin_bound : c->lin;
+  P.cfg = c->cfg;
+  P.u_old = c->u_old;
+  P.qp = c->qp;
+  P.nqp = c->nqp;
+  P.S = d.S;
+  P.p = d.p;
+  P.nu_tot = d.nu_tot;
+  P.ndist = d.ndist;
+  P.nd = L.nd;
+  P.rec_len = L.rec_len;
+  P.qp_len = c->qp_len;
+  P.off_A = L.off_A; P.off_B = L.off_B; P.off_C = L.off_C;
+  P.off_f = L.off_f; P.off_x = L.off_x; P.off_y = L.off_y;
+  P.nobs = L.nobs;
+  P.co = c->co;
+  int kd = 0, boff = d.ndist + L.nd, dmax = 1;
+  for (int i = 0; i < d.nu_tot; ++i) {
+    P.delay[i] = d.delay[i];
+    P.dindex[i] = -1;
+    if (d.delay[i] > 0) {
+      P.dindex[i] = kd;
+      P.dinput[kd] = i;
+      P.dlen[kd] = d.delay[i];
+      P.boff[kd] = boff;
+      boff += d.delay[i] - 1;
+      dmax = std::max(dmax, d.delay[i]);
+      ++kd;
+    }
+  }
+  P.dmax = dmax;
+  P.lds_per_wave = dmax * L.nd * (1 + d.ny);
+  if (P.lds_per_wave * CMPC_BUILD_WAVES * 8 > 64 * 1024) return fail("delays too long for LDS");
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
+  if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
+    return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
+  if (check_launch("build kernel")) return -1;
+  return timed_end(c, CMPC_KERNEL_BUILD, e0);
+}
+
+int cmpc_init_warmstart(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  if (ensure_cfg(c)) return -1;
+  HIP_TRY(hipSetDevice(c->device));
+  SolveParams P;
+  solve_params(c, &P);
+  P.init = 1;
+  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
+    return fail("solve kernel not instantiated for these dimensions");
+  return check_launch("init kernel");
+}
+
+int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
+  if (!c) return fail("null context");
+  if (K < 0) return fail("K must be >= 0");
+  if (ensure_cfg(c)) return -1;
+  HIP_TRY(hipSetDevice(c->device));
+  SolveParams P;
+  solve_params(c, &P);
+  P.K = K;
+  P.flags = flags;
+  if ((flags & CMPC_TRACE) && K > 0) {
+    const size_t need = (size_t)c->nqp * K * 16;
+    if (need > c->trace_cap) {
+      if (c->trace) HIP_TRY(hipFree(c->trace));
+      if (c->ntrace) HIP_TRY(hipFree(c->ntrace));
+      c->trace = nullptr;
+      c->ntrace = nullptr;
+      HIP_TRY(hipMalloc(&c->trace, need));
+      HIP_TRY(hipMalloc(&c->ntrace, sizeof(int32_t) * (size_t)c->nqp * K));
+      c->trace_cap = need;
+    }
+    P.trace = c->trace;
+    P.ntrace = c->ntrace;
+    c->trace_K = K;
+  }
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_ITERATE, &e0)) return -1;
+  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
+    return fail("solve kernel not instantiated for these dimensions");
+  if (check_launch("iterate kernel")) return -1;
+  return timed_end(c, CMPC_KERNEL_ITERATE, e0);
+}
+
+int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
+  if (cmpc_build(c)) return -1;
+  return cmpc_iterate(c, K, flags);
+}
+
+int cmpc_synchronize(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_download(cmpc_ctx* c, double* du, int32_t* status, int32_t* nwsr) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->nqp;
+  if (du) HIP_TRY(hipMemcpyAsync(du, c->du, sizeof(double) * n * c->L.nV, hipMemcpyDeviceToHost, c->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(status, c->status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  if (nwsr) HIP_TRY(hipMemcpyAsync(nwsr, c->nwsr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_download_qp(cmpc_ctx* c, double* H, double* f, double* G) {
+  if (!c) return fail("null context");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->nqp;
+  const int nV = c->L.nV, nVo = c->L.nVo;
+  std::vector<double> buf(n * c->qp_len);
+  HIP_TRY(hipMemcpyAsync(buf.data(), c->qp, sizeof(double) * buf.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t q = 0; q < n; ++q) {
+    const double* r = buf.data() + q * c->qp_len;
+    if (H) std::memcpy(H + q * nV * nV, r, sizeof(double) * nV * nV);
+    if (f) std::memcpy(f + q * nV, r + nV * nV, sizeof(double) * nV);
+    if (G && nVo) std::memcpy(G + q * nV * nVo, r + nV * nV + nV, sizeof(double) * nV * nVo);
+  }
+  return 0;
+}
+
+int cmpc_download_trace(cmpc_ctx* c, uint8_t* trace, int32_t* ntrace) {
+  if (!c) return fail("null context");
+  if (!c->trace) return fail("no traced iterate (pass CMPC_TRACE to cmpc_iterate)");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->nqp * c->trace_K;
+  if (trace) HIP_TRY(hipMemcpyAsync(trace, c->trace, n * 16, hipMemcpyDeviceToHost, c->stream));
+  if (ntrace) HIP_TRY(hipMemcpyAsync(ntrace, c->ntrace, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_enable_timing(cmpc_ctx* c, int enable) {
+  if (!c) return fail("null context");
+  if (resolve_timing(c)) return -1;
+  c->timing = enable != 0;
+  for (int k = 0; k < 2; ++k) {
+    c->tot_ms[k] = 0;
+    c->launches[k] = 0;
+  }
+  return 0;
+}
+
+int cmpc_kernel_time(cmpc_ctx* c, int kernel, double* total_ms, int64_t* launches) {
+  if (!c) return fail("null context");
+  if (kernel < 0 || kernel > 1) return fail("unknown kernel id");
+  HIP_TRY(hipSetDevice(c->device));
+  if (resolve_timing(c)) return -1;
+  if (total_ms) *total_ms = c->tot_ms[kernel];
+  if (launches) *launches = c->launches[kernel];
+  return 0;
+}
+
+int cmpc_qp_solve_batch(int device, int n, int nu, int nqp, const double* H, const double* g,
+                        const double* lb, const double* ub, const double* lbA, const double* ubA,
+                        const uint32_t* ws_in, int max_chg, double* x, int32_t* status,
+                        int32_t* nchg, uint32_t* ws_out, uint8_t* trace, int32_t* ntrace) {
+  if (nqp <= 0) return 0;
+  HIP_TRY(hipSetDevice(device));
+  const size_t q = (size_t)nqp;
+  double* dH; double* dg; double* dlb; double* dub; double* dlbA; double* dubA; double* dx;
+  uint32_t *dws, *dwo; int32_t *dst, *dnc, *dnt; uint8_t* dtr;
+  HIP_TRY(hipMalloc(&dH, sizeof(double) * q * n * n));
+  HIP_TRY(hipMalloc(&dg, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dlb, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dub, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dlbA, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dubA, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dx, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dws, sizeof(uint32_t) * q));
+  HIP_TRY(hipMalloc(&dwo, sizeof(uint32_t) * q));
+  HIP_TRY(hipMalloc(&dst, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dnc, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dnt, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dtr, 16 * q));
+  HIP_TRY(hipMemcpy(dH, H, sizeof(double) * q * n * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dg, g, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dlb, lb, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dub, ub, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dlbA, lbA, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dubA, ubA, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dws, ws_in, sizeof(uint32_t) * q, hipMemcpyHostToDevice));
+  QpBatchParams P{dH, dg, dlb, dub, dlbA, dubA, dws, dx, dst, dnc, dnt, dwo, dtr, nqp, max_chg};
+  if (cmpc_launch_qp_batch(P, n, nu, nullptr)) return fail("qp batch kernel not instantiated");
+  if (check_launch("qp batch kernel")) return -1;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(x, dx, sizeof(double) * q * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nchg, dnc, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ws_out, dwo, sizeof(uint32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(trace, dtr, 16 * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ntrace, dnt, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  void* bufs[] = {dH, dg, dlb, dub, dlbA, dubA, dx, dws, dwo, dst, dnc, dnt, dtr};
+  for (void* b : bufs) (void)hipFree(b);
+  return 0;
+}
+
+}  // extern "C"

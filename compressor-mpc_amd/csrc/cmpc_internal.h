@@ -1,0 +1,70 @@
+// Internal launch parameters shared by cmpc_abi.cpp (host) and
+// cmpc_kernels.hip (device).  Not part of the public ABI.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/cmpc.h"
+
+#define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
+#define CMPC_BUILD_WAVES 4       // QPs (= waves) per build workgroup
+#define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
+
+// Per sub-controller configuration block in device memory (doubles):
+//   [lwt  : ny*ny ]  L_W' with ywt = L_W L_W' (upper triangular)
+//   [yhat : p*ny  ]  L_W' y_ref_r
+//   [uwt  : nu*nu ]  input weight block of R = blkdiag_m(uwt)
+//   [lower, upper, rate_lower, rate_upper : nu each]
+struct CfgOffsets {
+  int lwt, yhat, uwt, lower, upper, rlower, rupper, len;
+};
+
+struct BuildParams {
+  const double* lin;     // nqp * rec_len
+  const double* cfg;     // S * cfg.len
+  const double* u_old;   // nqp * nu_tot
+  double* qp;            // nqp * qp_len   [H nV*nV | f nV | G nV*nVo]
+  int nqp, S, p, nu_tot, ndist, nd, dmax, rec_len, qp_len;
+  int off_A, off_B, off_C, off_f, off_x, off_y, nobs;
+  CfgOffsets co;
+  int delay[CMPC_MAX_INPUTS];    // per input
+  int dindex[CMPC_MAX_INPUTS];   // per input: delayed index kd or -1
+  int dinput[CMPC_ND_MAX];       // per delayed index: input c
+  int dlen[CMPC_ND_MAX];         // per delayed index: delay D
+  int boff[CMPC_ND_MAX];         // per delayed index: offset of its shift block in dx_aug
+  int lds_per_wave;              // doubles
+};
+
+struct SolveParams {
+  const double* qp;
+  const double* cfg;
+  double* u_old;      // nqp * nu_tot
+  double* du_old;     // nqp * nV
+  uint32_t* ws;       // nqp
+  double* du;         // nqp * nV
+  int32_t* status;    // nqp
+  int32_t* nwsr;      // nqp
+  uint8_t* trace;     // nqp * K * 16 or null
+  int32_t* ntrace;    // nqp * K or null
+  int nqp, S, K, nu_tot, qp_len;
+  CfgOffsets co;
+  uint32_t flags;
+  int init;           // 1: InitializeQPProblem (cold, f only, ws only)
+};
+
+// Standalone batched solver (parity / KKT tests).
+struct QpBatchParams {
+  const double *H, *g, *lb, *ub, *lbA, *ubA;
+  const uint32_t* ws_in;
+  double* x;
+  int32_t *status, *nchg, *ntrace;
+  uint32_t* ws_out;
+  uint8_t* trace;
+  int nqp, max_chg;
+};
+
+// Kernel launchers (cmpc_kernels.hip).  Return 0 or -1 (unsupported dims).
+int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
+                      void* stream);
+int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
+                      void* stream);
+int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);

@@ -1,0 +1,442 @@
+// Warm-started dual (Goldfarb–Idnani) active-set QP solver, one QP per
+// thread.  Same specification and arithmetic order as oracle/or_qp.c (see
+// DESIGN.md §QP).  Header-only and __host__ __device__ so that a CPU test
+// harness (tests/cpp/qp_host.cpp) can diff this exact code against the
+// oracle; the product only instantiates it inside the HIP kernels.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/cmpc.h"
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define CMPC_HD __host__ __device__ __forceinline__
+#else
+#define CMPC_HD inline
+#endif
+
+// ---------------------------------------------------------------------------
+// Warm-started dual active-set QP solver (lane per QP).  Same specification
+// and arithmetic order as oracle/or_qp.c; see DESIGN.md §QP.
+// ---------------------------------------------------------------------------
+#define TOL_P 1e-12
+#define TOL_D 1e-12
+#define TOL_R 1e-12
+#define TOL_Z 1e-12
+
+template <int N>
+CMPC_HD double sel(const double (&v)[N], int i) {
+  double r = 0.0;
+#pragma unroll
+  for (int t = 0; t < N; ++t) r = (i == t) ? v[t] : r;
+  return r;
+}
+
+template <int N, int NU>
+struct Qp {
+  double Hinv[N][N];
+  double lb[N], ub[N], lbA[N], ubA[N];
+
+  CMPC_HD double nu_dot(int j, int side, const double (&v)[N]) const {
+    double t;
+    if (j < N) {
+      t = sel<N>(v, j);
+    } else {
+      const int i = j - N;
+      t = (i >= NU) ? sel<N>(v, i) - sel<N>(v, i - NU) : sel<N>(v, i);
+    }
+    return side ? -t : t;
+  }
+  CMPC_HD void hinv_nu(int j, int side, double (&out)[N]) const {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double t;
+      if (j < N) {
+        t = sel<N>(Hinv[r], j);
+      } else {
+        const int i = j - N;
+        t = (i >= NU) ? sel<N>(Hinv[r], i) - sel<N>(Hinv[r], i - NU) : sel<N>(Hinv[r], i);
+      }
+      out[r] = side ? -t : t;
+    }
+  }
+  CMPC_HD double beta(int j, int side) const {
+    if (j < N) return side ? -sel<N>(ub, j) : sel<N>(lb, j);
+    return side ? -sel<N>(ubA, j - N) : sel<N>(lbA, j - N);
+  }
+};
+
+template <int N>
+struct WSet {
+  int K;
+  int j[N], side[N];
+  double lam[N];
+  double h[N][N];
+  double L[N][N], D[N];
+};
+
+// LDL' of the leading K x K block of M (M symmetric); returns false on a
+// non-positive pivot.
+template <int N>
+CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N],
+                                      double (&D)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j < K) {
+      double d = M[j][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
+      ok = ok && (d > 0.0);
+      D[j] = d;
+      L[j][j] = 1.0;
+#pragma unroll
+      for (int i = j + 1; i < N; ++i) {
+        if (i < K) {
+          double sacc = M[i][j];
+#pragma unroll
+          for (int k = 0; k < j; ++k) sacc = sacc - (L[i][k] * L[j][k]) * D[k];
+          L[i][j] = sacc / d;
+        }
+      }
+    }
+  }
+  return ok;
+}
+
+template <int N>
+CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
+                                            const double (&b)[N], double (&x)[N]) {
+  double y[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double v = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
+    y[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) y[i] = (i < K) ? y[i] / D[i] : 0.0;
+#pragma unroll
+  for (int i = N - 1; i >= 0; --i) {
+    if (i < K) {
+      double v = y[i];
+#pragma unroll
+      for (int k = i + 1; k < N; ++k)
+        if (k < K) v = v - L[k][i] * x[k];
+      x[i] = v;
+    } else {
+      x[i] = 0.0;
+    }
+  }
+}
+
+template <int N, int NU>
+CMPC_HD bool wset_factor(const Qp<N, NU>& q, WSet<N>& W) {
+  double M[N][N];
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+    if (a < W.K) q.hinv_nu(W.j[a], W.side[a], W.h[a]);
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+#pragma unroll
+    for (int b = a; b < N; ++b) {
+      double v = 0.0;
+      if (b < W.K) v = q.nu_dot(W.j[a], W.side[a], W.h[b]);
+      M[a][b] = v;
+      M[b][a] = v;
+    }
+  return ldl_k<N>(W.K, M, W.L, W.D);
+}
+
+template <int N>
+CMPC_HD void wset_drop(WSet<N>& W, int a) {
+#pragma unroll
+  for (int b = 0; b + 1 < N; ++b)
+    if (b >= a && b + 1 < W.K) {
+      W.j[b] = W.j[b + 1];
+      W.side[b] = W.side[b + 1];
+      W.lam[b] = W.lam[b + 1];
+    }
+  W.K--;
+}
+
+template <int N>
+CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam) {
+  int pos = 0;
+#pragma unroll
+  for (int b = 0; b < N; ++b)
+    if (b < W.K && W.j[b] < j) pos = b + 1;
+#pragma unroll
+  for (int b = N - 1; b > 0; --b)
+    if (b > pos && b <= W.K) {
+      W.j[b] = W.j[b - 1];
+      W.side[b] = W.side[b - 1];
+      W.lam[b] = W.lam[b - 1];
+    }
+#pragma unroll
+  for (int b = 0; b < N; ++b)
+    if (b == pos) {
+      W.j[b] = j;
+      W.side[b] = side;
+      W.lam[b] = lam;
+    }
+  W.K++;
+}
+
+struct QpOut {
+  int status, nchg, ntrace;
+  uint32_t ws;
+  uint32_t tr[4];  // 16 trace bytes
+};
+
+CMPC_HD void trace_push(QpOut& o, int add, int j, int side) {
+  if (o.ntrace < 16) {
+    const uint32_t byte = (add ? 0x80u : 0u) | (side ? 0x40u : 0u) | (uint32_t)j;
+    const int w = o.ntrace >> 2, sh = (o.ntrace & 3) * 8;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t == w) o.tr[t] = (o.tr[t] & ~(0xFFu << sh)) | (byte << sh);
+    o.ntrace++;
+  }
+}
+
+// Hinv = H^-1 via LDL' (oracle/or_qp.c step 0).  Returns false if not PD.
+template <int N>
+CMPC_HD bool hinv_of(const double (&H)[N][N], double (&Hinv)[N][N]) {
+  double L[N][N], D[N];
+  if (!ldl_k<N>(N, H, L, D)) return false;
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    double e[N], colv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = (i == c) ? 1.0 : 0.0;
+    ldl_solve_k<N>(N, L, D, e, colv);
+#pragma unroll
+    for (int i = 0; i <= c; ++i) Hinv[i][c] = colv[i];
+  }
+#pragma unroll
+  for (int c = 0; c < N; ++c)
+#pragma unroll
+    for (int i = 0; i < c; ++i) Hinv[c][i] = Hinv[i][c];
+  return true;
+}
+
+template <int N, int NU>
+CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&g)[N],
+                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
+  WSet<N> W;
+  o.status = CMPC_QP_OK;
+  o.nchg = 0;
+  o.ntrace = 0;
+  o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
+  W.K = 0;
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    W.j[a] = 0;
+    W.side[a] = 0;
+    W.lam[a] = 0.0;
+  }
+  int chg = 0;
+  bool done = false;
+  double xu[N];
+  if (!pd) {
+    o.status = CMPC_QP_NOT_PD;
+    done = true;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sacc = sacc + q.Hinv[i][j] * g[j];
+    xu[i] = -sacc;
+  }
+  // A. warm start
+  if (!done) {
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j)
+      if ((ws_in >> j) & 1u)
+        if (W.K < N) wset_add<N>(W, j, (ws_in >> (16 + j)) & 1u, 0.0);
+  }
+  for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
+    if (!wset_factor<N, NU>(q, W)) {
+      W.K = 0;
+      ++chg;
+      continue;
+    }
+    double rhs[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      rhs[a] = (a < W.K) ? q.beta(W.j[a], W.side[a]) - q.nu_dot(W.j[a], W.side[a], xu) : 0.0;
+    ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
+    int worst = -1;
+    double wv = -tol_d;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a < W.K && W.lam[a] < wv) {
+        wv = W.lam[a];
+        worst = a;
+      }
+    if (worst < 0) break;
+    int wj = 0, wsd = 0;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a == worst) {
+        wj = W.j[a];
+        wsd = W.side[a];
+      }
+    trace_push(o, 0, wj, wsd);
+    wset_drop<N>(W, worst);
+    if (++chg > max_chg) {
+      o.status = CMPC_QP_MAX_NWSR;
+      done = true;
+    }
+  }
+  if (!done) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double v = xu[r];
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a < W.K) v = v + W.lam[a] * W.h[a][r];
+      x[r] = v;
+    }
+  }
+  // B. Goldfarb–Idnani
+  for (int outer = 0; outer <= max_chg + 1 && !done; ++outer) {
+    int pj = -1, ps = 0;
+    double pv = 0.0;
+    uint32_t act = 0;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a < W.K) act |= 1u << W.j[a];
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j) {
+      if (!((act >> j) & 1u)) {
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          const double b = q.beta(j, sd);
+          const double sl = q.nu_dot(j, sd, x) - b;
+          if (sl < -TOL_P * (1.0 + fabs(b)) && (pj < 0 || sl < pv)) {
+            pj = j;
+            ps = sd;
+            pv = sl;
+          }
+        }
+      }
+    }
+    if (pj < 0) break;  // optimal
+    double up = 0.0;
+    for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
+      double hp[N], qv[N], rv[N], z[N];
+      q.hinv_nu(pj, ps, hp);
+#pragma unroll
+      for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? q.nu_dot(W.j[a], W.side[a], hp) : 0.0;
+      ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        double v = hp[r];
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          if (a < W.K) v = v - rv[a] * W.h[a][r];
+        z[r] = v;
+      }
+      const double zn = q.nu_dot(pj, ps, z);
+      const double den = q.nu_dot(pj, ps, hp);
+      int k = -1;
+      double t1 = 0.0;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a < W.K && rv[a] > TOL_R) {
+          const double ratio = W.lam[a] / rv[a];
+          if (k < 0 || ratio < t1) {
+            t1 = ratio;
+            k = a;
+          }
+        }
+      if (zn <= TOL_Z * den) {
+        if (k < 0) {
+          o.status = CMPC_QP_INFEASIBLE;
+          done = true;
+          break;
+        }
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          if (a < W.K) W.lam[a] = W.lam[a] - t1 * rv[a];
+        up = up + t1;
+        int kj = 0, ks = 0;
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          if (a == k) {
+            kj = W.j[a];
+            ks = W.side[a];
+          }
+        trace_push(o, 0, kj, ks);
+        wset_drop<N>(W, k);
+        if (++chg > max_chg) {
+          o.status = CMPC_QP_MAX_NWSR;
+          done = true;
+          break;
+        }
+        wset_factor<N, NU>(q, W);
+        continue;
+      }
+      const double sl = q.nu_dot(pj, ps, x) - q.beta(pj, ps);
+      const double t2 = -sl / zn;
+      const bool full = (k < 0) || (t2 <= t1);
+      const double t = full ? t2 : t1;
+#pragma unroll
+      for (int r = 0; r < N; ++r) x[r] = x[r] + t * z[r];
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a < W.K) W.lam[a] = W.lam[a] - t * rv[a];
+      up = up + t;
+      if (full) {
+        trace_push(o, 1, pj, ps);
+        wset_add<N>(W, pj, ps, up);
+        if (++chg > max_chg) {
+          o.status = CMPC_QP_MAX_NWSR;
+          done = true;
+          break;
+        }
+        wset_factor<N, NU>(q, W);
+        break;
+      }
+      int kj = 0, ks = 0;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a == k) {
+          kj = W.j[a];
+          ks = W.side[a];
+        }
+      trace_push(o, 0, kj, ks);
+      wset_drop<N>(W, k);
+      if (++chg > max_chg) {
+        o.status = CMPC_QP_MAX_NWSR;
+        done = true;
+        break;
+      }
+      wset_factor<N, NU>(q, W);
+    }
+  }
+  o.nchg = chg;
+  uint32_t w = 0;
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+    if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
+  o.ws = w;
+  if (o.status == CMPC_QP_OK) {
+    // variables at an active bound are fixed exactly at it
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a < W.K && W.j[a] < N) {
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+          if (r == W.j[a]) x[r] = W.side[a] ? q.ub[r] : q.lb[r];
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < N; ++r) x[r] = 0.0;
+  }
+}
+

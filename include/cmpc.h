@@ -134,6 +134,10 @@ int cmpc_get_state(cmpc_ctx* ctx, double* u_old, double* du_old, uint32_t* ws);
  * written in place by a device-side producer through cmpc_lin_device(). */
 int cmpc_upload_lin(cmpc_ctx* ctx, const double* lin_host);
 void* cmpc_lin_device(cmpc_ctx* ctx);
+/* Bind an external device-resident record array (B*S*rec_len doubles on the
+ * ctx device, e.g. the output of a device-side producer); NULL re-binds the
+ * context's own buffer.  Takes effect for the next cmpc_build. */
+int cmpc_bind_lin(cmpc_ctx* ctx, const double* lin_device);
 
 /* Hot path. */
 int cmpc_build(cmpc_ctx* ctx);
@@ -159,6 +163,17 @@ int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
 int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
 int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,
                      int64_t* launches);
+
+/* The batched QP solver alone, on device `device`, for host arrays of nqp
+ * QPs of size n (nu inputs per move): H nqp*n*n, g/lb/ub/lbA/ubA nqp*n,
+ * ws_in nqp; outputs x nqp*n, status/nchg nqp, ws_out nqp, trace nqp*16,
+ * ntrace nqp.  (Parity and known-answer tests of the solver.) */
+int cmpc_qp_solve_batch(int device, int n, int nu, int nqp, const double* H,
+                        const double* g, const double* lb, const double* ub,
+                        const double* lbA, const double* ubA,
+                        const uint32_t* ws_in, int max_chg, double* x,
+                        int32_t* status, int32_t* nchg, uint32_t* ws_out,
+                        uint8_t* trace, int32_t* ntrace);
 
 /* Upstream producer (host, untimed): AugmentedLinearizedSystem::Update for the
  * reference plants — linearise the plant at (x, u_full), discretise

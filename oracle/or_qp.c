@@ -209,7 +209,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
 
   /* A. warm start from ws_in */
   for (int j = 0; j < 2 * n; ++j)
-    if (ws_in & (1u << j)) wset_add(&W, j, (ws_in >> (16 + j)) & 1u, 0.0);
+    if ((ws_in & (1u << j)) && W.K < n) wset_add(&W, j, (ws_in >> (16 + j)) & 1u, 0.0);
   for (;;) {
     if (wset_factor(&q, &W)) { /* inconsistent warm start: cold */
       W.K = 0;

@@ -1,0 +1,84 @@
+"""The C-ABI library loads and exports every symbol include/cmpc.h declares;
+host-side (non-GPU) entry points agree with the oracle.  CPU only."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import cmpc
+from cmpc._abi import EXPORTS, CmpcDims, load_library
+from cmpc.configs import reference_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "cmpc.h")).read()
+    return set(re.findall(r"^\s*(?:int|void\*|const char\*)\s+(cmpc_\w+)\(", text, re.M))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == set(EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = load_library()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+@pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "ncoop", 50),
+                                           ("par", "cent", 200), ("ser", "coop", 100),
+                                           ("par", "coop", 20)])
+def test_layout_matches_oracle(plant, ctype, p):
+    cfg = reference_config(plant, ctype, p=p)
+    dims = CmpcDims.from_config(cfg, 7)
+    a, b = cmpc.layout_of(dims), O.layout(dims)
+    for f, _ in a._fields_:
+        assert getattr(a, f) == getattr(b, f), f
+    assert a.naug == 84 and a.nd == 2 and a.n_delay_states == 80
+
+
+def test_layout_rejects_bad_dims():
+    cfg = reference_config("par", "coop", p=50)
+    d = CmpcDims.from_config(cfg, 1)
+    d.m = 60  # m > p
+    L = cmpc.CmpcLayout() if hasattr(cmpc, "CmpcLayout") else None
+    from cmpc._abi import CmpcLayout
+    assert load_library().cmpc_layout_of(ctypes.byref(d), ctypes.byref(CmpcLayout())) != 0
+    assert b"invalid" in load_library().cmpc_last_error()
+
+
+@pytest.mark.parametrize("plant", [0, 1])
+def test_plant_producer_matches_oracle(plant):
+    """cmpc_plant_lin_record (product, host) == or_lin_record (oracle restatement)."""
+    rng = np.random.default_rng(7)
+    cfg = reference_config("par" if plant == 0 else "ser", "coop", p=20)
+    dims = CmpcDims.from_config(cfg, 1)
+    x0, u0 = cmpc.plant_default(plant)
+    xo, uo = O.plant_default(plant)
+    np.testing.assert_array_equal(x0, xo)
+    np.testing.assert_array_equal(u0, uo)
+    for trial in range(5):
+        x = x0 * (1 + 0.01 * rng.standard_normal(x0.shape))
+        u = u0.copy()
+        u[[0, 3, 4, 7]] += rng.uniform(-0.02, 0.02, 4)
+        np.testing.assert_allclose(cmpc.plant_output(plant, x), O.plant_output(plant, x),
+                                   rtol=1e-14, atol=0)
+        for s in range(cfg.S):
+            a = cmpc.plant_lin_record(cfg, dims, s, x, u)
+            b = O.lin_record(cfg, dims, s, x, u)
+            np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-14)
+
+
+def test_library_fails_loudly_without_device():
+    """No CPU fallback: creating a context without a HIP device is an error."""
+    from tests_util import no_gpu
+    if not no_gpu():
+        pytest.skip("a GPU is present")
+    cfg = reference_config("par", "coop", p=20)
+    with pytest.raises(RuntimeError):
+        cmpc.Context(cfg, 4)

