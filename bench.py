@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py — QP solves/sec (whole node) of the cooperative-parallel MPC hot
+path at horizon p = 50 (BASELINE.json metric) on MI355X.
+
+One step = one batched NerveCenter control step over B scenarios per GPU
+(2-compressor cooperative-parallel plant, S = 2 sub-controllers each, m = 2):
+condensed-QP build of every sub-controller (cmpc_build) + K = 9 Jacobi
+iterations of warm-started QP re-solves with the plan exchange
+(cmpc_iterate).  QP solves per step = B * S * K per GPU.
+
+Inputs are resident in HBM before the timed region: NB distinct synthetic
+batches are uploaded once and step i binds batch i % NB,
+so consecutive steps solve different QPs while the warm-start working sets
+persist, as in the reference's closed loop.
+
+Multi-GPU: one process per GPU (torch.distributed.run), scenarios sharded
+across ranks with no data-path collective (weak scaling); the barrier and
+the max-over-ranks of the elapsed time use torch.distributed (RCCL).
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
+
+import numpy as np  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix), spec
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_flops(cfg, naug: int, nd: int) -> float:
+    """Algorithmic FLOPs of one sub-controller build (FMA = 2)."""
+    p, ny, ns, nu_tot, nV = cfg.p, cfg.ny, cfg.ns, cfg.nu_tot, cfg.nV
+    return (p * 2 * ny * ns * (ns + nd) + p * 2 * ny * ns * (nu_tot - nd) + p * ny * nu_tot +
+            p * ny * ns + 2 * p * ny * ny * nV + 2 * nV * nV * p * ny +
+            2 * p * ny * (ns + naug) + p * ny + 2 * p * ny * nV)
+
+
+def build_bytes(cfg, L) -> float:
+    """Algorithmic HBM bytes of one sub-controller build: its lin record
+    (Aorig, Bin, Csel, f, dx_aug, y_prev) + u_old in, the condensed QP out."""
+    ns, ny, nu_tot = cfg.ns, cfg.ny, cfg.nu_tot
+    rec = ns * ns + ns * nu_tot + ny * L.nobs + ns + L.naug + ny
+    out = L.nV * L.nV + L.nV + L.nV * L.nVo
+    return 8.0 * (rec + nu_tot + out)
+
+
+def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
+    """The oracle (CPU restatement of the reference path: O(p^2) Su loop,
+    dense products, the build's active-set solver) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    from cmpc._abi import CmpcDims
+    S = cfg.S
+
+    def run(nb, th, reps):
+        dims = CmpcDims.from_config(cfg, nb)
+        sl = slice(0, nb * S)
+        lin_s = np.ascontiguousarray(lin[sl])
+        u_s = np.ascontiguousarray(u_old[sl])
+        du_s = np.zeros((nb * S, cfg.nV))
+        ws_s = np.zeros(nb * S, np.uint32)
+        O.step(dims, arrays, lin_s, K, u_s.copy(), du_s.copy(), ws_s.copy(), init=True, threads=th)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.step(dims, arrays, lin_s, K, u_s, du_s, ws_s, threads=th)
+        return (time.perf_counter() - t0) / reps
+
+    probe = min(64, lin.shape[0] // S)
+    t1 = run(probe, threads, 1)
+    nb = int(min(lin.shape[0] // S, max(probe, probe * target_s / max(t1, 1e-6))))
+    t_pass = run(nb, threads, 1)
+    reps = max(1, int(round(target_s / max(t_pass, 1e-6))))
+    dt = run(nb, threads, reps)
+    t_single = run(probe, 1, 1)
+    return {
+        "value": nb * S * K / dt,
+        "seconds": dt * reps,
+        "unit": "QP solves/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{reps} control steps of {nb} scenarios x {S} sub-controllers x K={K} "
+                   f"Jacobi iterations (build + solves) of batch 0, oracle/liboracle.so "
+                   f"(reference op order, -O3, OpenMP), {dt * reps:.1f} s"),
+        "single_thread_value": probe * S * K / t_single,
+        "single_thread_us_per_scenario_step": t_single / probe * 1e6,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="scenarios per GPU")
+    ap.add_argument("--p", type=int, default=50)
+    ap.add_argument("--K", type=int, default=9)
+    ap.add_argument("--input-batches", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world}, --gpus={args.gpus}; using WORLD_SIZE")
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.synthetic import synthetic_batch
+
+    cfg = cmpc.reference_config("par", "coop", p=args.p)
+    arrays = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    B, S, K, NB = args.batch, cfg.S, args.K, args.input_batches
+    t0 = time.time()
+    batches = []
+    u_old = du_old = ws = None
+    for b in range(NB):
+        lin, u, du, w = synthetic_batch(cfg, B, seed=1002 + 101 * rank + b, n_distinct=min(B, 2048))
+        if b == 0:
+            u_old, du_old, ws, lin0 = u, du, w, lin
+        batches.append(torch.from_numpy(lin).to(f"cuda:{local}"))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] synthetic inputs: {NB} x {B} scenarios in {time.time() - t0:.1f} s")
+
+    ctx = cmpc.Context(cfg, B, device=local)
+    ctx.configure(arrays)
+    ctx.set_state(u_old, du_old, ws)
+    ctx.bind_lin(batches[0].data_ptr())
+    ctx.build()
+    ctx.init_warmstart()
+    for i in range(args.warmup):
+        ctx.bind_lin(batches[i % NB].data_ptr())
+        ctx.step(K, 0)
+    ctx.synchronize()
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.enable_timing(True)
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ctx.bind_lin(batches[(args.warmup + i) % NB].data_ptr())
+        ctx.step(K, 0)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        dist.barrier()
+    build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+    iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    du, st, nw = ctx.download()
+    _, _, ws_now = ctx.get_state()
+    ok_frac = float((st == 0).mean())
+    active_frac = float((ws_now != 0).mean())
+    mean_chg = float(nw.mean())
+
+    solves = world * B * S * K * args.steps
+    value = solves / elapsed_max
+    L = ctx.layout
+    avg_build_s = build_ms / max(n_build, 1) / 1e3
+    f_build = build_flops(cfg, L.naug, L.nd)
+    achieved_tf = B * S * f_build / avg_build_s / 1e12
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_build_coop_p50.json")
+    if os.path.exists(pmc):
+        try:
+            rec = json.load(open(pmc))
+            if rec.get("batch") == B:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "QP solves/sec (whole node), cooperative-parallel MPC, horizon p=50",
+        "value": value,
+        "unit": "QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8(d) recipe, seeded; resident in HBM)",
+        "config": {
+            "workload": (f"cooperative-parallel, 2 compressors, p={cfg.p}, m={cfg.m}, "
+                         f"S={S} sub-controllers, K={K} Jacobi iterations, {B} scenarios/GPU"),
+            "global_batch": world * B,
+            "qp_per_gpu": B * S,
+            "p": cfg.p, "m": cfg.m, "S": S, "K": K,
+            "input_batches": NB,
+            "parallelism": f"scenario-sharded replicas x{world} (no data-path collective)",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "pipe": "fp64 VALU (v_fmac_f64_dpp); MI355X FP64 vector peak = FP64 matrix peak",
+            "kernel": "cmpc_build_kernel<11,3,2,2>",
+            "achieved": achieved_tf,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_PEAK_TFLOPS,
+            "traffic": traffic,
+            "flops_per_qp": f_build,
+            "algorithmic_bytes_per_qp": build_bytes(cfg, L),
+            "avg_launch_ms": avg_build_s * 1e3,
+            "launches": n_build,
+        },
+        "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
+                                "iterate": iter_ms / max(n_iter, 1)},
+        "qp_status_ok_fraction": ok_frac,
+        "qp_active_constraint_fraction": active_frac,
+        "mean_working_set_changes_last_solve": mean_chg,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        try:
+            out["cpu_baseline"] = cpu_baseline(cfg, arrays, lin0, u_old, K, args.cpu_seconds, threads)
+        except Exception as e:  # the baseline is reported, never required
+            log(f"cpu baseline failed: {e}")
+            out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,3 +143,43 @@ class SetupFile:
         out.rate_lower = num("constraints-rate-lower")
         out.rate_upper = num("constraints-rate-upper")
         return out
+
+
+# Run parameters of the reference's setup files (setup/setup-<ctrl>-<plant>,
+# values copied as data; n-iterations is the Jacobi iteration count K).
+_REF_SETUPS = {
+    ("par", "cent"): dict(n_iterations=1, yref=[4.5, 4.5, 0, 1.12],
+                          uwt=[2e4, 2e5, 2e4, 2e5], ywt=[[1, 1, 5e2]],
+                          lo=[-0.3, 0, -0.3, 0], up=[0.3, 1, 0.3, 1],
+                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1]),
+    ("par", "coop"): dict(n_iterations=9, yref=[4.5, 4.5, 0, 1.12],
+                          uwt=[1.9e4, 1.9e5, 1.9e4, 1.9e5], ywt=[[1, 1, 4.2e2]] * 2,
+                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+    ("par", "ncoop"): dict(n_iterations=9, yref=[4.5, 4.5, 0, 1.12],
+                           uwt=[2.2e4, 2.2e5, 2.2e4, 2.2e5], ywt=[[1, 6e2]] * 2,
+                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+    ("ser", "cent"): dict(n_iterations=1, yref=[1.030830, 8.125790, 1.187190, 8.125790],
+                          uwt=[2e4, 2.5e5, 2e4, 2.5e5], ywt=[[200, 1, 1000, 8]],
+                          lo=[-0.3, 0, -0.3, 0], up=[0.3, 1, 0.3, 1],
+                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1]),
+    ("ser", "coop"): dict(n_iterations=9, yref=[1.030830, 8.125790, 1.187190, 8.125790],
+                          uwt=[4.1e4, 5e5, 2.5e4, 5e5], ywt=[[750, 4, 1500, 8]] * 2,
+                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+    ("ser", "ncoop"): dict(n_iterations=9, yref=[1.030830, 8.125790, 1.187190, 8.125790],
+                           uwt=[3e4, 5e5, 3e4, 5e5], ywt=[[1900, 3]] * 2,
+                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+}
+
+
+def reference_setup(plant: str, controller: str) -> SetupFile:
+    """The reference's setup file for (plant, controller) as a SetupFile
+    (diagonal weight matrices expanded)."""
+    key = ({"parallel": "par", "serial": "ser"}.get(plant, plant),
+           {"centralized": "cent", "cooperative": "coop", "noncoop": "ncoop"}.get(controller, controller))
+    v = _REF_SETUPS[key]
+    diag = lambda d: [float(d[i]) if i == j else 0.0 for i in range(len(d)) for j in range(len(d))]
+    return SetupFile(n_iterations=v["n_iterations"], n_timing_iterations=v["n_iterations"],
+                     yref=[float(t) for t in v["yref"]], uwt=diag(v["uwt"]),
+                     ywt=[diag(w) for w in v["ywt"]], constraints_lower=list(map(float, v["lo"])),
+                     constraints_upper=list(map(float, v["up"])),
+                     rate_lower=list(map(float, v["rlo"])), rate_upper=list(map(float, v["rup"])))

@@ -10,7 +10,12 @@ Per scenario b (seed = 1000 + config_id unless given):
   derivative ~ 1/sqrt|dp| explodes; the nominal radius is 0.995)
 Per QP slot (scenario b, sub-controller s):
   dx_aug tail ~ N(0, 1e-3)
-  u_old: torque inputs ~ U(-0.05, 0.05), recycle inputs ~ U(0, 0.05)
+  u_old: torque inputs ~ U(-0.098, 0.074), recycle inputs 0 (closed, at its
+         lower bound) with probability 0.1, else U(0, 0.066) — calibrated to
+         the reference's closed-loop records (results/parallel/run1/coop9.dat:
+         torque in [-0.0977, 0.0739], recycle in [0, 0.0656], recycle == 0 in
+         10.0% of the 10 000 steps); the survey recipe (U(-0.05,0.05), U(0,0.05))
+         leaves only ~5% of QPs with an active constraint
   y_prev = plant output at x_b (controlled entries)
   du_old = 0, ws = 0
 """
@@ -60,7 +65,10 @@ def synthetic_batch(cfg: ControllerConfig, B: int, seed: int = 1002, n_distinct:
     for s in range(S):
         for c, plant_c in enumerate(cfg.input_order[s]):
             torque = plant_c in (0, 2)     # control inputs: torque1, rec1, torque2, rec2
-            u_old[:, s, c] = (rng.uniform(-0.05, 0.05, B) if torque else rng.uniform(0.0, 0.05, B))
+            if torque:
+                u_old[:, s, c] = rng.uniform(-0.098, 0.074, B)
+            else:
+                u_old[:, s, c] = np.where(rng.random(B) < 0.1, 0.0, rng.uniform(0.0, 0.066, B))
     u_old = np.ascontiguousarray(u_old.reshape(nq, cfg.nu_tot))
     du_old = np.zeros((nq, cfg.nV))
     ws = np.zeros(nq, np.uint32)

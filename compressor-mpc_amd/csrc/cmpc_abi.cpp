@@ -89,6 +89,7 @@ struct cmpc_ctx {
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
+  std::vector<hipEvent_t> event_pool;  // reused so timing stays cheap in a timed loop
   double tot_ms[2] = {0, 0};
   int64_t launches[2] = {0, 0};
 };
@@ -152,18 +153,27 @@ int rebuild_cfg(cmpc_ctx* c) {
 
 int ensure_cfg(cmpc_ctx* c) { return c->cfg_dirty ? rebuild_cfg(c) : 0; }
 
+hipError_t pooled_event(cmpc_ctx* c, hipEvent_t* e) {
+  if (!c->event_pool.empty()) {
+    *e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreate(e);
+}
+
 int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
-  if (!c->timing) return 0;
-  HIP_TRY(hipEventCreate(e0));
-  HIP_TRY(hipEventRecord(*e0, c->stream));
   (void)k;
+  if (!c->timing) return 0;
+  HIP_TRY(pooled_event(c, e0));
+  HIP_TRY(hipEventRecord(*e0, c->stream));
   return 0;
 }
 
 int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
   if (!c->timing) return 0;
   hipEvent_t e1;
-  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(pooled_event(c, &e1));
   HIP_TRY(hipEventRecord(e1, c->stream));
   c->pending[k].push_back({e0, e1});
   c->launches[k]++;
@@ -177,8 +187,8 @@ int resolve_timing(cmpc_ctx* c) {
       float ms = 0;
       HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
       c->tot_ms[k] += ms;
-      (void)hipEventDestroy(pr.first);
-      (void)hipEventDestroy(pr.second);
+      c->event_pool.push_back(pr.first);
+      c->event_pool.push_back(pr.second);
     }
     c->pending[k].clear();
   }
@@ -302,6 +312,7 @@ int cmpc_destroy(cmpc_ctx* c) {
       (void)hipEventDestroy(pr.first);
       (void)hipEventDestroy(pr.second);
     }
+  for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
                   c->ws,  c->status, c->nwsr, c->trace, c->ntrace};
   for (void* b : bufs)
@@ -457,8 +468,29 @@ int cmpc_build(cmpc_ctx* c) {
     }
   }
   P.dmax = dmax;
-  P.lds_per_wave = dmax * L.nd * (1 + d.ny);
-  if (P.lds_per_wave * CMPC_BUILD_WAVES * 8 > 64 * 1024) return fail("delays too long for LDS");
+  {
+    const int ndw = L.nd > 0 ? L.nd : 1;
+    const int nvm = L.nV * d.m;
+    P.lds_block = d.S * (d.p + 1) * d.ny + d.S * d.ny * d.ny + d.S * d.nu * d.nu + 16;
+    P.lds_block = (P.lds_block + 1) / 2 * 2;
+    // must match the kernel's per-wave layout (cmpc_kernels.hip, U = 4)
+    P.lds_per_wave = L.rec_len + 8 + d.ny * L.nobs + 4 + (d.p + 2) * ndw +
+                     std::max(L.nd * d.ny * (dmax + d.p), (d.ny - 1) * (d.nu_tot + 1) * nvm) +
+                     (d.nu_tot + 2) * d.ny * 4;
+    P.lds_per_wave = (P.lds_per_wave + 1) / 2 * 2;  // 16-byte aligned wave regions
+  }
+  if (L.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return fail("lin record too long for the build kernel");
+  const size_t lds_bytes = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
+  if (lds_bytes > 64 * 1024) return fail("horizon/delays too long for the build kernel's LDS");
+  {
+    // persistent grid: the launcher caps this at (resident workgroups per CU,
+    // from the occupancy query: registers and LDS) x CUs, so no workgroup
+    // waits for a second round
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    P.cus = cus;
+    P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
+  }
   hipEvent_t e0 = nullptr;
   if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
   if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))

@@ -6,7 +6,8 @@
 #include "../../include/cmpc.h"
 
 #define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
-#define CMPC_BUILD_WAVES 4       // QPs (= waves) per build workgroup
+#define CMPC_BUILD_WAVES 4       // waves per build workgroup (one QP per wave at a time)
+#define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 #define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
 
 // Per sub-controller configuration block in device memory (doubles):
@@ -31,7 +32,10 @@ struct BuildParams {
   int dinput[CMPC_ND_MAX];       // per delayed index: input c
   int dlen[CMPC_ND_MAX];         // per delayed index: delay D
   int boff[CMPC_ND_MAX];         // per delayed index: offset of its shift block in dx_aug
-  int lds_per_wave;              // doubles
+  int lds_block;                 // doubles of block-shared LDS (yhat of all sub-controllers)
+  int lds_per_wave;              // doubles of per-wave LDS (record, w, ring)
+  int grid;                      // workgroups needed (one QP per wave); launcher caps it
+  int cus;                       // compute units of the device
 };
 
 struct SolveParams {

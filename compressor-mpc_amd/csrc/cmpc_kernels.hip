@@ -1,3 +1,4 @@
+#include <algorithm>
 // MI355X (gfx950) kernels of the condensed-QP hot path.
 //
 // build  : AdjustAllDelayedStates + GeneratePrediction + GenerateDistributedQP
@@ -31,172 +32,294 @@
 // ---------------------------------------------------------------------------
 // build kernel
 // ---------------------------------------------------------------------------
-template <int NS, int NY, int NU, int M>
+template <int NS, int NY, int NU, int M, int ND>
 __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
+  constexpr int NVM = NV * M;
+  constexpr int NDW = ND > 0 ? ND : 1;
+  constexpr int NCH = CMPC_REC_CHUNKS;  // 16-byte record chunks per lane
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int q_raw = blockIdx.x * CMPC_BUILD_WAVES + wave;
-  const bool active = q_raw < P.nqp;
-  const int q = active ? q_raw : P.nqp - 1;
   const int row = lane >> 4, col = lane & 15;
-  const int s = q % P.S;
-  const int nu_tot = P.nu_tot, ND = P.nd, Dmax = P.dmax;
-  const double* rec = P.lin + (size_t)q * P.rec_len;
-  const double* cfg = P.cfg + (size_t)s * P.co.len;
-  const double* uold = P.u_old + (size_t)q * nu_tot;
-  const double* lwt = cfg + P.co.lwt;
-  double* wl = smem + wave * P.lds_per_wave;  // w[t*ND + k]
-  double* ring = wl + Dmax * ND;              // ring[(kd*NY + o)*Dmax + pos]
+  const int nu_tot = P.nu_tot, Dmax = P.dmax, pp = P.p, S = P.S;
+  const int nobs = P.nobs, rec_len = P.rec_len;
+  const int nwaves = gridDim.x * CMPC_BUILD_WAVES;
+  const int nchunk = rec_len / 2;
 
-  // delay-line inputs, AdjustAllDelayedStates applied (include/aug_lin_sys.h:141-154)
-  for (int e = lane; e < Dmax * ND; e += 64) {
-    const int t = e / ND, k = e - t * ND;
-    double v = 0.0;
-    if (t < P.dlen[k]) {
-      const double x = (t == 0) ? rec[P.off_x + P.ndist + k] : rec[P.off_x + P.boff[k] + t - 1];
-      v = x - uold[P.dinput[k]];
-    }
-    wl[e] = v;
+  // ---- LDS layout (doubles) ----
+  // block: [yhat S x (p+1) x NY][lwt S x NY x NY][uwt S x NU x NU][zeros 16]
+  // wave : [rec rec_len][uold 8][chat NY x nobs][kappa 4][w (p+2) x NDW]
+  //        [delay lines ND x NY x (Dmax + p)][hand-off slots (nu_tot+2) x NY x U]
+  //        (the row reduction reuses the delay-line area after the loop)
+  double* yl_all = smem;
+  double* lw_all = yl_all + S * (pp + 1) * NY;
+  double* uw_all = lw_all + S * NY * NY;
+  double* zeros = uw_all + S * NU * NU;
+  double* recl = smem + P.lds_block + wave * P.lds_per_wave;
+  const int o_uold = rec_len, o_chat = o_uold + 8, o_kap = o_chat + NY * nobs;
+  constexpr int U = 4;  // horizon-loop unroll (immediate LDS offsets)
+  const int dl_len = Dmax + pp;
+  const int o_w = o_kap + 4, o_ring = o_w + (pp + 2) * NDW;
+  const int o_slot = o_ring + max(ND * NY * dl_len, (NY - 1) * (nu_tot + 1) * NVM);
+  double* uol = recl + o_uold;
+  double* chat = recl + o_chat;
+  double* kap = recl + o_kap;
+  double* wl = recl + o_w;
+  double* ring = recl + o_ring;
+  double* slots = recl + o_slot;
+  double* red = ring;
+  for (int e = threadIdx.x; e < S * (pp + 1) * NY; e += 64 * CMPC_BUILD_WAVES) {
+    const int ss = e / ((pp + 1) * NY), t = e - ss * (pp + 1) * NY;
+    yl_all[e] = (t < pp * NY) ? P.cfg[(size_t)ss * P.co.len + P.co.yhat + t] : 0.0;
   }
-  for (int e = lane; e < ND * NY * Dmax; e += 64) ring[e] = 0.0;
+  for (int e = threadIdx.x; e < S * NY * NY; e += 64 * CMPC_BUILD_WAVES)
+    lw_all[e] = P.cfg[(size_t)(e / (NY * NY)) * P.co.len + P.co.lwt + e % (NY * NY)];
+  for (int e = threadIdx.x; e < S * NU * NU; e += 64 * CMPC_BUILD_WAVES)
+    uw_all[e] = P.cfg[(size_t)(e / (NU * NU)) * P.co.len + P.co.uwt + e % (NU * NU)];
+  if (threadIdx.x < 16) zeros[threadIdx.x] = 0.0;
   __syncthreads();
 
-  const int nobs = P.nobs;
-  const double* A = rec + P.off_A;
-  const double* Bin = rec + P.off_B;
-  const double* Cs = rec + P.off_C;
-  const double* xh = rec + P.off_f;
+  // ---- static lane roles and LDS gather descriptors (same for every QP) ----
   const bool prow = row < NY;
   const bool srow = row == 3;
-
-  // per-lane operands of the broadcast FMA
-  double m[NS];
-  double pv = 0.0, xadd = 0.0;
-  double ad[CMPC_ND_MAX];
-#pragma unroll
-  for (int k = 0; k < CMPC_ND_MAX; ++k) ad[k] = 0.0;
-#pragma unroll
-  for (int l = 0; l < NS; ++l) {
-    double v = 0.0;
-    if (prow) {
-      if (col < NS) v = A[l * NS + col];
-      else if (col < NS + nu_tot) v = Bin[l * nu_tot + (col - NS)];
-    } else if (srow) {
-      if (col < NS) {
-        v = A[col * NS + l];
-      } else if (col < NS + NY) {
-        const int o = col - NS;
-        for (int o2 = o; o2 < NY; ++o2) v += lwt[o * NY + o2] * Cs[o2 * nobs + l];
-      }
-    }
-    m[l] = v;
-  }
-  if (prow && col < NS) {
-    for (int o2 = row; o2 < NY; ++o2) pv += lwt[row * NY + o2] * Cs[o2 * nobs + col];
-  }
-  if (srow && col < NS) {
-    for (int k = 0; k < ND && k < CMPC_ND_MAX; ++k) ad[k] = Bin[col * nu_tot + P.dinput[k]];
-    xadd = xh[col];
-    double x1 = xh[col];
-    for (int k = 0; k < ND && k < CMPC_ND_MAX; ++k) x1 += ad[k] * wl[k];
-    pv = x1;  // x_1 = f + Adelay w_0  (x_0 = 0)
-  }
-  if (srow && col >= NS && col < NS + NY) {
-    const int o = col - NS;
-    const double* xa = rec + P.off_x;
-    const double* yp = rec + P.off_y;
-    for (int o2 = o; o2 < NY; ++o2) {
-      double dist = 0.0;
-      for (int d = 0; d < P.ndist; ++d) dist += Cs[o2 * nobs + NS + d] * xa[d];
-      xadd += lwt[o * NY + o2] * (dist + yp[o2]);
-    }
-  }
-
-  // Markov / z lanes
   const int c_in = col - NS;
   const bool mlane = prow && col >= NS && col < NS + nu_tot;
   const bool zlane = prow && col == NS + nu_tot;
   const int D = mlane ? P.delay[c_in] : 0;
   const int kd = mlane ? P.dindex[c_in] : -1;
   const bool rlane = mlane && D > 0;
-  double* rbase = ring + (rlane ? (kd * NY + row) * Dmax : 0);
-  int rpos = 0;
-  double hist[M], ssum = 0.0;
-#pragma unroll
-  for (int k = 0; k < M; ++k) hist[k] = 0.0;
-  double acc[NV * M];
-#pragma unroll
-  for (int k = 0; k < NV * M; ++k) acc[k] = 0.0;
-  const double* yhat = cfg + P.co.yhat;
   const int oz = (col >= NS && col < NS + NY) ? col - NS : 0;
-  const int zsrc = 48 + NS + (row < NY ? row : 0);
+  const double ym = (srow && col >= NS && col < NS + NY) ? 1.0 : 0.0;
+  const double* zero_p = zeros;
+  // m[l] = mb[l * ms]
+  const double* mb = zero_p;
+  int ms = 0;
+  if (prow && col < NS) { mb = recl + P.off_A + col; ms = NS; }
+  else if (mlane) { mb = recl + P.off_B + c_in; ms = nu_tot; }
+  else if (srow && col < NS) { mb = recl + P.off_A + col * NS; ms = 1; }
+  else if (srow && col < NS + NY) { mb = chat + oz * nobs; ms = 1; }
+  // initial broadcast source and chain base
+  const double* pv_src = (prow && col < NS) ? chat + row * nobs + col
+                         : (srow && col < NS) ? recl + P.off_f + col : zero_p;
+  const double* base_src = (srow && col < NS) ? recl + P.off_f + col
+                           : (srow && col < NS + NY) ? kap + oz : zero_p;
+  const double* ad_src = (srow && col < NS) ? recl + P.off_B + col * nu_tot : zero_p;
+  // Hand-off through LDS, one masked write + read per step:
+  //   delayed Markov lanes: delay line, write at Dmax + r, read at Dmax + r - D
+  //   undelayed Markov lanes: own slot (read back what was just written)
+  //   sim output lanes write z_r[o]; the z lane of row o reads it
+  const bool slane = srow && col >= NS && col < NS + NY;
+  const bool hand = mlane || zlane || slane;
+  double* wp = slots;
+  const double* rp = slots;
+  int hinc = 0;
+  if (rlane) {
+    wp = ring + (kd * NY + row) * dl_len + Dmax;
+    rp = wp - D;
+    hinc = U;
+  } else if (mlane) {
+    wp = slots + (row * nu_tot + c_in) * U;
+    rp = wp;
+  } else if (slane) {
+    wp = slots + (NY * nu_tot + oz) * U;
+  } else if (zlane) {
+    wp = slots + (NY * nu_tot + NY + row) * U;  // private scratch slot (write unused)
+    rp = slots + (NY * nu_tot + row) * U;
+  }
+  // reduction: rows 1..NY-1 of the Markov/z lanes park their sums in LDS
+  const bool red_lane = (row >= 1 && row < NY) && col >= NS && col <= NS + nu_tot;
+  double* red_w = red + (((row >= 1 ? row : 1) - 1) * (nu_tot + 1) + (col >= NS ? c_in : 0)) * NVM;
 
-  for (int r = 0; r < P.p; ++r) {
-    double a0 = 0.0, a1 = 0.0;
-    prop_dpp<NS>(pv, m, a0, a1);
-    const double qv = a0 + a1;
-    double simx = qv + xadd;
-    if (r + 1 < Dmax) {
+  // ---- prefetch the first record (coalesced 16-byte loads) ----
+  int q = blockIdx.x * CMPC_BUILD_WAVES + wave;
+  double2 chunk[NCH];
 #pragma unroll
-      for (int k = 0; k < CMPC_ND_MAX; ++k)
-        if (k < ND) simx += ad[k] * wl[(r + 1) * ND + k];
-    }
-    const double zq = qv + xadd - yhat[r * NY + oz];
-    pv = srow ? simx : qv;
-    double hv = qv;
-    if (rlane) {
-      const double old = rbase[rpos];
-      rbase[rpos] = qv;
-      hv = old;
-      rpos = (rpos + 1 == D) ? 0 : rpos + 1;
-    }
-    const double zval = __shfl(zq, zsrc, 64);
+  for (int i = 0; i < NCH; ++i) {
+    const int ci = lane + 64 * i;
+    chunk[i] = (q < P.nqp && ci < nchunk)
+                   ? reinterpret_cast<const double2*>(P.lin + (size_t)q * rec_len)[ci]
+                   : make_double2(0.0, 0.0);
+  }
+  double uold_l = (q < P.nqp && lane < nu_tot) ? P.u_old[(size_t)q * nu_tot + lane] : 0.0;
+
+  for (; q < P.nqp; q += nwaves) {
+    const int s = q % S;
+    const double* yl = yl_all + s * (pp + 1) * NY;
+    const double* lwt = lw_all + s * NY * NY;
+    // record -> LDS, then issue the next record's loads
 #pragma unroll
-    for (int k = M - 1; k > 0; --k) hist[k] = hist[k - 1];
-    hist[0] = hv;
-    ssum += hist[M - 1];
-    double v[M];
-#pragma unroll
-    for (int k = 0; k < M; ++k) {
-      const double mv = (k < M - 1) ? hist[k] : ssum;
-      v[k] = mlane ? mv : ((zlane && k == 0) ? zval : 0.0);
+    for (int i = 0; i < NCH; ++i) {
+      const int ci = lane + 64 * i;
+      if (ci < nchunk) reinterpret_cast<double2*>(recl)[ci] = chunk[i];
     }
-    accum_dpp<NS, NU, M>(v, acc);
+    if (lane < nu_tot) uol[lane] = uold_l;
+    {
+      const int qn = q + nwaves;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int ci = lane + 64 * i;
+        chunk[i] = (qn < P.nqp && ci < nchunk)
+                       ? reinterpret_cast<const double2*>(P.lin + (size_t)qn * rec_len)[ci]
+                       : make_double2(0.0, 0.0);
+      }
+      uold_l = (qn < P.nqp && lane < nu_tot) ? P.u_old[(size_t)qn * nu_tot + lane] : 0.0;
+    }
+    const double* Cs = recl + P.off_C;
+    const double* xa = recl + P.off_x;
+    // C_hat = L_W' C_sel (ny x nobs), one element per lane
+    if (prow && col < nobs) {
+      double t = 0.0;
+#pragma unroll
+      for (int o2 = 0; o2 < NY; ++o2)
+        if (o2 >= row) t += lwt[row * NY + o2] * Cs[o2 * nobs + col];
+      chat[row * nobs + col] = t;
+    }
+    // delay-line inputs w_t, AdjustAllDelayedStates applied (include/aug_lin_sys.h:141-154)
+    for (int e = lane; e < (pp + 2) * NDW; e += 64) {
+      const int t = e / NDW, k = e - t * NDW;
+      double v = 0.0;
+      if (k < ND && t < P.dlen[k]) {
+        const double x = (t == 0) ? xa[P.ndist + k] : xa[P.boff[k] + t - 1];
+        v = x - uol[P.dinput[k]];
+      }
+      wl[e] = v;
+    }
+    for (int e = lane; e < ND * NY * Dmax; e += 64) {
+      const int li = e / Dmax;
+      ring[li * dl_len + (e - li * Dmax)] = 0.0;  // zero history before t = 0
+    }
+    // kappa = L_W'(dist + y_prev) = C_hat_dist xa_dist + L_W' y_prev
+    if (prow && col == 15) {
+      const double* yp = recl + P.off_y;
+      double t = 0.0;
+      for (int d = 0; d < P.ndist; ++d) t += chat[row * nobs + NS + d] * xa[d];
+#pragma unroll
+      for (int o2 = 0; o2 < NY; ++o2)
+        if (o2 >= row) t += lwt[row * NY + o2] * yp[o2];
+      kap[row] = t;
+    }
+    // per-lane operands (branch-free gathers through the descriptors)
+    double m[NS];
+#pragma unroll
+    for (int l = 0; l < NS; ++l) m[l] = mb[l * ms];
+    double ad[NDW];
+#pragma unroll
+    for (int k = 0; k < NDW; ++k) ad[k] = (ND > 0) ? ad_src[ms == 1 ? P.dinput[k] : 0] : 0.0;
+    const double base = *base_src;
+    double pv = *pv_src;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) pv += ad[k] * wl[k];  // sim: x_1 = f + Adelay w_0
+
+    double acc[NVM];
+#pragma unroll
+    for (int k = 0; k < NVM; ++k) acc[k] = 0.0;
+    double hist[M], ssum = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) hist[k] = 0.0;
+    double yh = yl[oz];
+    double wn[NDW];
+#pragma unroll
+    for (int k = 0; k < NDW; ++k) wn[k] = (ND > 0) ? wl[NDW + k] : 0.0;
+    double bp = 0.0;
+    double* wq = wp;
+    const double* rq = rp;
+    const double* wlp = wl + 2 * NDW;
+    const double* ylp = yl + NY + oz;
+
+    // one horizon step; u = position inside the unrolled group (immediate offsets)
+#define CMPC_BUILD_STEP(u)                                                             \
+  {                                                                                    \
+    /* chain init: sim lanes f + Adelay w_{r+1}; z lanes kappa - yhat_r; P rows 0 */  \
+    double a = __builtin_fma(-ym, yh, base);                                           \
+    _Pragma("unroll") for (int k = 0; k < ND; ++k) a = __builtin_fma(ad[k], wn[k], a); \
+    prop1_dpp<NS>(pv, m, a);                                                           \
+    /* accumulate row r-1 (its hand-off landed a step ago) */                          \
+    _Pragma("unroll") for (int k = M - 1; k > 0; --k) hist[k] = hist[k - 1];          \
+    hist[0] = bp;                                                                      \
+    ssum += hist[M - 1];                                                               \
+    double va[M];                                                                      \
+    _Pragma("unroll") for (int k = 0; k < M; ++k) va[k] = (k < M - 1) ? hist[k] : ssum; \
+    accum_dpp<NS, NU, M>(va, acc);                                                     \
+    _Pragma("unroll") for (int k = 0; k < NDW; ++k) wn[k] = (ND > 0) ? wlp[(u) * NDW + k] : 0.0; \
+    yh = ylp[(u) * NY];                                                                \
+    /* a: P rows -> P_{r+1} / raw Markov; sim lanes -> x_{r+2}; z lanes -> z_r */      \
+    pv = a;                                                                            \
+    if (hand) {                                                                        \
+      wq[u] = a;                                                                       \
+      bp = rq[u];                                                                      \
+    }                                                                                  \
   }
 
-  // reduce over the ny rows and store row 0 of lanes ns .. ns + nu_tot
-  double tot[NV * M];
-#pragma unroll
-  for (int k = 0; k < NV * M; ++k) {
-    double t = acc[k];
-    for (int o = 1; o < NY; ++o) t += __shfl(acc[k], (lane + 16 * o) & 63, 64);
-    tot[k] = t;
-  }
-  if (active && row == 0 && col >= NS && col <= NS + nu_tot) {
-    double* out = P.qp + (size_t)q * P.qp_len;
-    const int c = col - NS;
-    const int nuo = nu_tot - NU, nVo = M * nuo;
-    const double* uwt = cfg + P.co.uwt;
-    if (c < NU) {
-#pragma unroll
-      for (int a = 0; a < NV; ++a)
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          const int b = k * NU + c;
-          const double rw = (a / NU == k) ? uwt[(a % NU) * NU + c] : 0.0;
-          out[a * NV + b] = tot[a * M + k] + rw;
-        }
-    } else if (c < nu_tot) {
-#pragma unroll
-      for (int a = 0; a < NV; ++a)
-#pragma unroll
-        for (int k = 0; k < M; ++k) out[NV * NV + NV + a * nVo + k * nuo + (c - NU)] = tot[a * M + k];
-    } else {
-#pragma unroll
-      for (int a = 0; a < NV; ++a) out[NV * NV + a] = tot[a * M];
+    int r = 0;
+    for (; r + U <= pp; r += U) {
+      CMPC_BUILD_STEP(0)
+      CMPC_BUILD_STEP(1)
+      CMPC_BUILD_STEP(2)
+      CMPC_BUILD_STEP(3)
+      wq += hinc;
+      rq += hinc;
+      wlp += U * NDW;
+      ylp += U * NY;
     }
+    for (; r < pp; ++r) {
+      CMPC_BUILD_STEP(0)
+      wq += hinc / U;
+      rq += hinc / U;
+      wlp += NDW;
+      ylp += NY;
+    }
+#undef CMPC_BUILD_STEP
+    {
+#pragma unroll
+      for (int k = M - 1; k > 0; --k) hist[k] = hist[k - 1];
+      hist[0] = bp;
+      ssum += hist[M - 1];
+      double va[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) va[k] = (k < M - 1) ? hist[k] : ssum;
+      accum_dpp<NS, NU, M>(va, acc);  // row p-1
+    }
+    // note: the accumulation of row -1 at r = 0 adds products of zeros
+
+    // reduce over the ny rows through LDS; row 0 of lanes ns .. ns + nu_tot stores
+    if (red_lane) {
+#pragma unroll
+      for (int k = 0; k < NVM; ++k) red_w[k] = acc[k];
+    }
+    if (row == 0 && col >= NS && col <= NS + nu_tot) {
+      double tot[NVM];
+#pragma unroll
+      for (int k = 0; k < NVM; ++k) tot[k] = acc[k];
+#pragma unroll
+      for (int o = 1; o < NY; ++o) {
+        const double* rr = red + ((o - 1) * (nu_tot + 1) + c_in) * NVM;
+#pragma unroll
+        for (int k = 0; k < NVM; ++k) tot[k] += rr[k];
+      }
+      double* out = P.qp + (size_t)q * P.qp_len;
+      const int c = c_in;
+      const int nuo = nu_tot - NU, nVo = M * nuo;
+      const double* uwt = uw_all + s * NU * NU;
+      if (c < NU) {
+#pragma unroll
+        for (int a = 0; a < NV; ++a)
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const double rw = (a / NU == k) ? uwt[(a % NU) * NU + c] : 0.0;
+            out[a * NV + k * NU + c] = tot[a * M + k] + rw;
+          }
+      } else if (c < nu_tot) {
+#pragma unroll
+        for (int a = 0; a < NV; ++a)
+#pragma unroll
+          for (int k = 0; k < M; ++k) out[NV * NV + NV + a * nVo + k * nuo + (c - NU)] = tot[a * M + k];
+      } else {
+#pragma unroll
+        for (int a = 0; a < NV; ++a) out[NV * NV + a] = tot[a * M];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -352,10 +475,16 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
 // launchers — explicit instantiation list (cf. the reference's *_list.h)
 // ---------------------------------------------------------------------------
 #define BUILD_CASE(NS_, NY_, NU_, M_)                                                  \
-  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_) {                                \
-    const int grid = (P.nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES;                \
-    const size_t lds = sizeof(double) * (size_t)P.lds_per_wave * CMPC_BUILD_WAVES;     \
-    hipLaunchKernelGGL((cmpc_build_kernel<NS_, NY_, NU_, M_>), dim3(grid),             \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2) {                   \
+    const size_t lds = sizeof(double) * ((size_t)P.lds_block +                         \
+                                         (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);  \
+    int per_cu = 1;                                                                    \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
+            &per_cu, cmpc_build_kernel<NS_, NY_, NU_, M_, 2>, 64 * CMPC_BUILD_WAVES,  \
+            lds) != hipSuccess || per_cu < 1)                                         \
+      per_cu = 1;                                                                      \
+    const int grid = std::max(1, std::min(P.grid, P.cus * per_cu));                   \
+    hipLaunchKernelGGL((cmpc_build_kernel<NS_, NY_, NU_, M_, 2>), dim3(grid),           \
                        dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                        \
     return 0;                                                                          \
   }

@@ -59,3 +59,18 @@ def test_parallel_recycle_at_lower_bound():
                         np.zeros((cfg.S, cfg.nV)), np.zeros(cfg.S, np.uint32), init=True)
         u = plant_input_from_plans(cfg, du.reshape(1, cfg.S, cfg.nV))[0]
         assert u[1] == 0.0 and u[3] == 0.0
+
+
+@pytest.mark.parametrize("name", GC.NAMES)
+def test_product_reference_setups_match_setup_files(name):
+    """cmpc.configs.reference_setup restates setup/setup-<ctrl>-<plant> (fixture)."""
+    from cmpc.configs import reference_setup
+    cfg, setup, arr, g = GC.case(name)
+    ctype, plant = name.split("-")
+    mine = reference_setup(plant, ctype)
+    assert mine.n_iterations == g["n_iterations"]
+    assert mine.yref == g["yref"] and mine.uwt == g["uwt"]
+    assert [v for blk in mine.ywt for v in blk][:len(g["ywt"])] == g["ywt"]
+    assert mine.constraints_lower == g["constraints_lower"]
+    assert mine.constraints_upper == g["constraints_upper"]
+    assert mine.rate_lower == g["rate_lower"] and mine.rate_upper == g["rate_upper"]
