@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Copy the rocprofv3 summaries of one GPU round into profiles/ (tracked).
+
+usage: python tools/summarize_profiles.py TAG ROUND [BATCH]
+
+  gpurun_out/prof_TAG/run_kernel_stats.csv      -> profiles/ROUND_kernel_stats.csv
+  gpurun_out/pmcTAG_{sq1,sq2,fetch,write}/...   -> profiles/ROUND_pmc.json
+                                                 + profiles/pmc_build_coop_p50.json
+
+HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of a 16-byte-per-lane coalesced streaming read (the build kernel's record
+loads are exactly that), so it is doubled; WRITE_SIZE is taken as is.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def counters(tag, name):
+    path = os.path.join(OUT, f"pmc{tag}_{name}", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    acc = defaultdict(lambda: defaultdict(list))
+    for row in csv.DictReader(open(path)):
+        acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} | {"_dispatches": len(next(iter(d.values())))}
+            for k, d in acc.items()}
+
+
+def main():
+    tag, rnd = sys.argv[1], sys.argv[2]
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+    os.makedirs(PROF, exist_ok=True)
+    ks = os.path.join(OUT, f"prof_{tag}", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(PROF, f"{rnd}_kernel_stats.csv"))
+        print("copied", ks)
+    merged = defaultdict(dict)
+    for name in ("sq1", "sq2", "fetch", "write"):
+        for k, d in counters(tag, name).items():
+            merged[k].update(d)
+    if not merged:
+        return
+    summary = {"note": __doc__.strip().splitlines()[0], "batch_scenarios": batch, "kernels": {}}
+    for k, d in merged.items():
+        e = dict(d)
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            e["hbm_read_bytes"] = 2.0 * d["FETCH_SIZE"] * 1024.0
+            e["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024.0
+            e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+        if "SQ_WAVES" in d and d["SQ_WAVES"]:
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+                if c in d:
+                    e[c + "_per_wave"] = d[c] / d["SQ_WAVES"]
+        if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+                if c in d:
+                    e[c + "_frac"] = d[c] / d["SQ_WAVE_CYCLES"]
+        summary["kernels"][k] = e
+    json.dump(summary, open(os.path.join(PROF, f"{rnd}_pmc.json"), "w"), indent=1)
+    b = summary["kernels"].get("cmpc_build_kernel", {})
+    if "hbm_bytes_per_launch" in b:
+        json.dump({"batch": batch, "round": rnd, "kernel": "cmpc_build_kernel",
+                   "hbm_bytes_per_launch": b["hbm_bytes_per_launch"],
+                   "hbm_read_bytes": b["hbm_read_bytes"], "hbm_write_bytes": b["hbm_write_bytes"],
+                   "source": f"profiles/{rnd}_pmc.json"},
+                  open(os.path.join(PROF, "pmc_build_coop_p50.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
