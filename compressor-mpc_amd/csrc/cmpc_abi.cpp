@@ -238,6 +238,7 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
     return fail("nu_tot must equal S * nu (each sub-controller owns nu inputs)");
   if (L.nd > CMPC_ND_MAX) return fail("more than 4 delayed inputs");
   if (d.ns + d.nu_tot > 15) return fail("ns + nu_tot must be <= 15 (16-lane DPP rows)");
+  if (d.m * d.nu_tot + 1 > 16) return fail("m * nu_tot + 1 must be <= 16 (gather lanes of a DPP row)");
   if (d.ny > 3) return fail("ny > 3 is not instantiated in the build kernel");
   const long long nqp = (long long)d.B * d.S;
   if (nqp > (1LL << 30)) return fail("batch too large");
@@ -469,19 +470,21 @@ int cmpc_build(cmpc_ctx* c) {
   }
   P.dmax = dmax;
   {
-    const int ndw = L.nd > 0 ? L.nd : 1;
-    const int nvm = L.nV * d.m;
     P.lds_block = d.S * (d.p + 1) * d.ny + d.S * d.ny * d.ny + d.S * d.nu * d.nu + 16;
     P.lds_block = (P.lds_block + 1) / 2 * 2;
-    // must match the kernel's per-wave layout (cmpc_kernels.hip, U = 4)
-    P.lds_per_wave = L.rec_len + 8 + d.ny * L.nobs + 4 + (d.p + 2) * ndw +
-                     std::max(L.nd * d.ny * (dmax + d.p), (d.ny - 1) * (d.nu_tot + 1) * nvm) +
-                     (d.nu_tot + 2) * d.ny * 4;
+    // must match the kernel's per-wave layout (cmpc_kernels.hip)
+    int rowlen = 0;
+    for (int c = 0; c < d.nu_tot; ++c) rowlen += d.delay[c] + d.m - 1 + d.p;
+    rowlen += rowlen & 1;
+    const int ng = d.m * d.nu_tot + 1;
+    const int head = L.rec_len + 8 + d.ny * L.nobs + 4;  // record, u_old, C_hat, kappa
+    const int lines = (std::max(std::max(d.ny * rowlen, (d.ny - 1) * ng * L.nV), head) + 1) / 2 * 2;
+    P.lds_per_wave = lines + ((d.p + 3) * d.ny + 1) / 2 * 2 + d.ny * 4 + 64 + 4;
     P.lds_per_wave = (P.lds_per_wave + 1) / 2 * 2;  // 16-byte aligned wave regions
   }
   if (L.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return fail("lin record too long for the build kernel");
   const size_t lds_bytes = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
-  if (lds_bytes > 64 * 1024) return fail("horizon/delays too long for the build kernel's LDS");
+  if (lds_bytes > 160 * 1024) return fail("horizon/delays too long for the build kernel's LDS");
   {
     // persistent grid: the launcher caps this at (resident workgroups per CU,
     // from the occupancy query: registers and LDS) x CUs, so no workgroup

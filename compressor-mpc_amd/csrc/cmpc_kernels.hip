@@ -32,43 +32,59 @@
 // ---------------------------------------------------------------------------
 // build kernel
 // ---------------------------------------------------------------------------
-template <int NS, int NY, int NU, int M, int ND>
+template <int NS, int NY, int NUT, int NU, int M, int ND>
 __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
-  constexpr int NVM = NV * M;
+  constexpr int NG = M * NUT + 1;  // gather lanes per row: QP columns (move k, input c), then z
   constexpr int NDW = ND > 0 ? ND : 1;
   constexpr int NCH = CMPC_REC_CHUNKS;  // 16-byte record chunks per lane
+  constexpr int U = 4;                  // horizon-loop unroll (immediate LDS offsets)
+  static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
+  static_assert(ND <= NY, "w table shares the yhat stride");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int row = lane >> 4, col = lane & 15;
-  const int nu_tot = P.nu_tot, Dmax = P.dmax, pp = P.p, S = P.S;
+  const int pp = P.p, S = P.S;
   const int nobs = P.nobs, rec_len = P.rec_len;
   const int nwaves = gridDim.x * CMPC_BUILD_WAVES;
   const int nchunk = rec_len / 2;
 
+  // Delay lines: one per (row o, input c), length D_c + M - 1 + p; the first
+  // D_c + M - 1 entries are zero (history before t = 0), raw Markov value of
+  // step r at index D_c + M - 1 + r.  Reading index (M - 1 - k) + r yields the
+  // column (move k, input c) of row r for every c: the delay shifts out.
+  int coff[NUT], rowlen = 0;
+#pragma unroll
+  for (int c = 0; c < NUT; ++c) {
+    coff[c] = rowlen;
+    rowlen += P.delay[c] + M - 1 + pp;
+  }
+  rowlen += rowlen & 1;  // 16-byte aligned rows
+
   // ---- LDS layout (doubles) ----
   // block: [yhat S x (p+1) x NY][lwt S x NY x NY][uwt S x NU x NU][zeros 16]
-  // wave : [rec rec_len][uold 8][chat NY x nobs][kappa 4][w (p+2) x NDW]
-  //        [delay lines ND x NY x (Dmax + p)][hand-off slots (nu_tot+2) x NY x U]
-  //        (the row reduction reuses the delay-line area after the loop)
+  // wave : [rec rec_len][uold 8][chat NY x nobs][kappa 4]   (prologue only)
+  //        overlaid by [delay lines NY x rowlen] (horizon loop), then by the
+  //        row reduction (epilogue); followed by
+  //        [w (p+3) x NY][z slots NY x U][scratch 64 + U]
   double* yl_all = smem;
   double* lw_all = yl_all + S * (pp + 1) * NY;
   double* uw_all = lw_all + S * NY * NY;
   double* zeros = uw_all + S * NU * NU;
   double* recl = smem + P.lds_block + wave * P.lds_per_wave;
   const int o_uold = rec_len, o_chat = o_uold + 8, o_kap = o_chat + NY * nobs;
-  constexpr int U = 4;  // horizon-loop unroll (immediate LDS offsets)
-  const int dl_len = Dmax + pp;
-  const int o_w = o_kap + 4, o_ring = o_w + (pp + 2) * NDW;
-  const int o_slot = o_ring + max(ND * NY * dl_len, (NY - 1) * (nu_tot + 1) * NVM);
+  const int o_line = 0;
+  const int o_w = (max(max(NY * rowlen, (NY - 1) * NG * NV), o_kap + 4) + 1) / 2 * 2;
+  const int o_zl = o_w + ((pp + 3) * NY + 1) / 2 * 2;
   double* uol = recl + o_uold;
   double* chat = recl + o_chat;
   double* kap = recl + o_kap;
   double* wl = recl + o_w;
-  double* ring = recl + o_ring;
-  double* slots = recl + o_slot;
-  double* red = ring;
+  double* lines = recl + o_line;
+  double* zl = recl + o_zl;
+  double* scratch = zl + NY * U;  // write target of lanes without a hand-off role
+  double* red = lines;
   for (int e = threadIdx.x; e < S * (pp + 1) * NY; e += 64 * CMPC_BUILD_WAVES) {
     const int ss = e / ((pp + 1) * NY), t = e - ss * (pp + 1) * NY;
     yl_all[e] = (t < pp * NY) ? P.cfg[(size_t)ss * P.co.len + P.co.yhat + t] : 0.0;
@@ -84,52 +100,49 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
   const bool prow = row < NY;
   const bool srow = row == 3;
   const int c_in = col - NS;
-  const bool mlane = prow && col >= NS && col < NS + nu_tot;
-  const bool zlane = prow && col == NS + nu_tot;
-  const int D = mlane ? P.delay[c_in] : 0;
-  const int kd = mlane ? P.dindex[c_in] : -1;
-  const bool rlane = mlane && D > 0;
-  const int oz = (col >= NS && col < NS + NY) ? col - NS : 0;
-  const double ym = (srow && col >= NS && col < NS + NY) ? 1.0 : 0.0;
+  const bool mlane = prow && col >= NS && col < NS + NUT;       // raw Markov writer
+  const bool slane = srow && col >= NS && col < NS + NY;        // free-response writer
+  const bool glane = prow && col < NG;                          // gather (accumulating) lane
+  const bool wlane = srow && col >= 16 - ND;                    // delayed-input carrier lane
+  const int oz = slane ? col - NS : 0;
+  const int kw = wlane ? col - (16 - ND) : 0;
+  const double ym = slane ? 1.0 : wlane ? -1.0 : 0.0;
   const double* zero_p = zeros;
   // m[l] = mb[l * ms]
   const double* mb = zero_p;
   int ms = 0;
   if (prow && col < NS) { mb = recl + P.off_A + col; ms = NS; }
-  else if (mlane) { mb = recl + P.off_B + c_in; ms = nu_tot; }
+  else if (mlane) { mb = recl + P.off_B + c_in; ms = NUT; }
   else if (srow && col < NS) { mb = recl + P.off_A + col * NS; ms = 1; }
-  else if (srow && col < NS + NY) { mb = chat + oz * nobs; ms = 1; }
+  else if (slane) { mb = chat + oz * nobs; ms = 1; }
   // initial broadcast source and chain base
   const double* pv_src = (prow && col < NS) ? chat + row * nobs + col
-                         : (srow && col < NS) ? recl + P.off_f + col : zero_p;
+                         : (srow && col < NS) ? recl + P.off_f + col
+                         : wlane ? wl + NY + kw : zero_p;
   const double* base_src = (srow && col < NS) ? recl + P.off_f + col
-                           : (srow && col < NS + NY) ? kap + oz : zero_p;
-  const double* ad_src = (srow && col < NS) ? recl + P.off_B + col * nu_tot : zero_p;
-  // Hand-off through LDS, one masked write + read per step:
-  //   delayed Markov lanes: delay line, write at Dmax + r, read at Dmax + r - D
-  //   undelayed Markov lanes: own slot (read back what was just written)
-  //   sim output lanes write z_r[o]; the z lane of row o reads it
-  const bool slane = srow && col >= NS && col < NS + NY;
-  const bool hand = mlane || zlane || slane;
-  double* wp = slots;
-  const double* rp = slots;
-  int hinc = 0;
-  if (rlane) {
-    wp = ring + (kd * NY + row) * dl_len + Dmax;
-    rp = wp - D;
-    hinc = U;
-  } else if (mlane) {
-    wp = slots + (row * nu_tot + c_in) * U;
-    rp = wp;
-  } else if (slane) {
-    wp = slots + (NY * nu_tot + oz) * U;
-  } else if (zlane) {
-    wp = slots + (NY * nu_tot + NY + row) * U;  // private scratch slot (write unused)
-    rp = slots + (NY * nu_tot + row) * U;
+                           : slane ? kap + oz : zero_p;
+  const double* ad_src = (srow && col < NS) ? recl + P.off_B + col * NUT : zero_p;
+  // hand-off: writers store their chain value of step r, gather lanes read
+  // the QP column values of row r (one masked LDS write + read per step)
+  // (delay-line pointers advance one entry per step, z slots are reused)
+  double* wp = scratch + lane;
+  int winc = 0, rinc = 0;
+  if (mlane) { wp = lines + row * rowlen + coff[c_in] + P.delay[c_in] + M - 1; winc = 1; }
+  else if (slane) wp = zl + oz * U;
+  const double* rp = zero_p;
+  double smask = 0.0;  // 1: running-sum column (move M-1)
+  if (glane) {
+    if (col < M * NUT) {
+      const int k = col / NUT, c = col - k * NUT;
+      rp = lines + row * rowlen + coff[c] + (M - 1 - k);
+      smask = (k == M - 1) ? 1.0 : 0.0;
+      rinc = 1;
+    } else {
+      rp = zl + row * U;
+    }
   }
-  // reduction: rows 1..NY-1 of the Markov/z lanes park their sums in LDS
-  const bool red_lane = (row >= 1 && row < NY) && col >= NS && col <= NS + nu_tot;
-  double* red_w = red + (((row >= 1 ? row : 1) - 1) * (nu_tot + 1) + (col >= NS ? c_in : 0)) * NVM;
+  const bool red_lane = (row >= 1 && row < NY) && col < NG;
+  double* red_w = red + ((row >= 1 ? row - 1 : 0) * NG + col) * NV;
 
   // ---- prefetch the first record (coalesced 16-byte loads) ----
   int q = blockIdx.x * CMPC_BUILD_WAVES + wave;
@@ -141,7 +154,7 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
                    ? reinterpret_cast<const double2*>(P.lin + (size_t)q * rec_len)[ci]
                    : make_double2(0.0, 0.0);
   }
-  double uold_l = (q < P.nqp && lane < nu_tot) ? P.u_old[(size_t)q * nu_tot + lane] : 0.0;
+  double uold_l = (q < P.nqp && lane < NUT) ? P.u_old[(size_t)q * NUT + lane] : 0.0;
 
   for (; q < P.nqp; q += nwaves) {
     const int s = q % S;
@@ -153,7 +166,7 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
       const int ci = lane + 64 * i;
       if (ci < nchunk) reinterpret_cast<double2*>(recl)[ci] = chunk[i];
     }
-    if (lane < nu_tot) uol[lane] = uold_l;
+    if (lane < NUT) uol[lane] = uold_l;
     {
       const int qn = q + nwaves;
 #pragma unroll
@@ -163,7 +176,7 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
                        ? reinterpret_cast<const double2*>(P.lin + (size_t)qn * rec_len)[ci]
                        : make_double2(0.0, 0.0);
       }
-      uold_l = (qn < P.nqp && lane < nu_tot) ? P.u_old[(size_t)qn * nu_tot + lane] : 0.0;
+      uold_l = (qn < P.nqp && lane < NUT) ? P.u_old[(size_t)qn * NUT + lane] : 0.0;
     }
     const double* Cs = recl + P.off_C;
     const double* xa = recl + P.off_x;
@@ -175,19 +188,16 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
         if (o2 >= row) t += lwt[row * NY + o2] * Cs[o2 * nobs + col];
       chat[row * nobs + col] = t;
     }
-    // delay-line inputs w_t, AdjustAllDelayedStates applied (include/aug_lin_sys.h:141-154)
-    for (int e = lane; e < (pp + 2) * NDW; e += 64) {
-      const int t = e / NDW, k = e - t * NDW;
+    // delay-line inputs w_t (stride NY), AdjustAllDelayedStates applied
+    // (include/aug_lin_sys.h:141-154); zero once the delay line has drained
+    for (int e = lane; e < (pp + 3) * NY; e += 64) {
+      const int t = e / NY, k = e - t * NY;
       double v = 0.0;
       if (k < ND && t < P.dlen[k]) {
         const double x = (t == 0) ? xa[P.ndist + k] : xa[P.boff[k] + t - 1];
         v = x - uol[P.dinput[k]];
       }
       wl[e] = v;
-    }
-    for (int e = lane; e < ND * NY * Dmax; e += 64) {
-      const int li = e / Dmax;
-      ring[li * dl_len + (e - li * Dmax)] = 0.0;  // zero history before t = 0
     }
     // kappa = L_W'(dist + y_prev) = C_hat_dist xa_dist + L_W' y_prev
     if (prow && col == 15) {
@@ -200,55 +210,48 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
       kap[row] = t;
     }
     // per-lane operands (branch-free gathers through the descriptors)
-    double m[NS];
+    // m[NS + k] = Adelay[j][k]: the sim row's state lanes pick up w_{r+1}
+    // from the carrier lanes 16 - ND + k inside the DPP chain
+    double m[NS + NDW];
 #pragma unroll
     for (int l = 0; l < NS; ++l) m[l] = mb[l * ms];
-    double ad[NDW];
 #pragma unroll
-    for (int k = 0; k < NDW; ++k) ad[k] = (ND > 0) ? ad_src[ms == 1 ? P.dinput[k] : 0] : 0.0;
+    for (int k = 0; k < NDW; ++k) m[NS + k] = (ND > 0) ? ad_src[ms == 1 ? P.dinput[k] : 0] : 0.0;
     const double base = *base_src;
     double pv = *pv_src;
 #pragma unroll
-    for (int k = 0; k < ND; ++k) pv += ad[k] * wl[k];  // sim: x_1 = f + Adelay w_0
+    for (int k = 0; k < ND; ++k) pv += m[NS + k] * wl[k];  // sim: x_1 = f + Adelay w_0
 
-    double acc[NVM];
+    // zero the delay lines (their first D_c + M - 1 entries are the history
+    // before t = 0; the rest is overwritten by the loop); the record area
+    // they overlay is dead once the operands above are in registers
+    for (int e = lane; e < (NY * rowlen + 1) / 2; e += 64)
+      reinterpret_cast<double2*>(lines)[e] = make_double2(0.0, 0.0);
+    double acc[NV];
 #pragma unroll
-    for (int k = 0; k < NVM; ++k) acc[k] = 0.0;
-    double hist[M], ssum = 0.0;
-#pragma unroll
-    for (int k = 0; k < M; ++k) hist[k] = 0.0;
-    double yh = yl[oz];
-    double wn[NDW];
-#pragma unroll
-    for (int k = 0; k < NDW; ++k) wn[k] = (ND > 0) ? wl[NDW + k] : 0.0;
-    double bp = 0.0;
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    double va = 0.0;  // gather lane: QP column value of the previous row
+    double rd = 0.0;  // gather lane: raw value read at the end of the previous step
+    // per-step operand: yhat_r (output lanes) / w_{r+2} (carrier lanes)
+    double yh = wlane ? wl[2 * NY + kw] : yl[oz];
+    const double* ylp = wlane ? wl + 3 * NY + kw : yl + NY + oz;
     double* wq = wp;
     const double* rq = rp;
-    const double* wlp = wl + 2 * NDW;
-    const double* ylp = yl + NY + oz;
 
     // one horizon step; u = position inside the unrolled group (immediate offsets)
 #define CMPC_BUILD_STEP(u)                                                             \
   {                                                                                    \
-    /* chain init: sim lanes f + Adelay w_{r+1}; z lanes kappa - yhat_r; P rows 0 */  \
+    /* chain init: f (states), kappa - yhat_r (outputs), w_{r+2} (carriers) */         \
     double a = __builtin_fma(-ym, yh, base);                                           \
-    _Pragma("unroll") for (int k = 0; k < ND; ++k) a = __builtin_fma(ad[k], wn[k], a); \
-    prop1_dpp<NS>(pv, m, a);                                                           \
-    /* accumulate row r-1 (its hand-off landed a step ago) */                          \
-    _Pragma("unroll") for (int k = M - 1; k > 0; --k) hist[k] = hist[k - 1];          \
-    hist[0] = bp;                                                                      \
-    ssum += hist[M - 1];                                                               \
-    double va[M];                                                                      \
-    _Pragma("unroll") for (int k = 0; k < M; ++k) va[k] = (k < M - 1) ? hist[k] : ssum; \
-    accum_dpp<NS, NU, M>(va, acc);                                                     \
-    _Pragma("unroll") for (int k = 0; k < NDW; ++k) wn[k] = (ND > 0) ? wlp[(u) * NDW + k] : 0.0; \
+    prop1w_dpp<NS, ND>(pv, m, a);                                                      \
+    /* accumulate row r-1: acc[a] += column_a * own column (gather lanes) */          \
+    va = __builtin_fma(smask, va, rd);                                                 \
+    gacc_dpp<NUT, NU, M>(va, acc);                                                     \
     yh = ylp[(u) * NY];                                                                \
-    /* a: P rows -> P_{r+1} / raw Markov; sim lanes -> x_{r+2}; z lanes -> z_r */      \
+    /* a: P rows -> P_{r+1} / raw Markov of step r; sim lanes -> x_{r+2} / z_r */      \
     pv = a;                                                                            \
-    if (hand) {                                                                        \
-      wq[u] = a;                                                                       \
-      bp = rq[u];                                                                      \
-    }                                                                                  \
+    wq[u] = a;                                                                         \
+    rd = rq[u];                                                                        \
   }
 
     int r = 0;
@@ -257,66 +260,52 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
       CMPC_BUILD_STEP(1)
       CMPC_BUILD_STEP(2)
       CMPC_BUILD_STEP(3)
-      wq += hinc;
-      rq += hinc;
-      wlp += U * NDW;
+      wq += U * winc;
+      rq += U * rinc;
       ylp += U * NY;
     }
     for (; r < pp; ++r) {
       CMPC_BUILD_STEP(0)
-      wq += hinc / U;
-      rq += hinc / U;
-      wlp += NDW;
+      wq += winc;
+      rq += rinc;
       ylp += NY;
     }
 #undef CMPC_BUILD_STEP
-    {
-#pragma unroll
-      for (int k = M - 1; k > 0; --k) hist[k] = hist[k - 1];
-      hist[0] = bp;
-      ssum += hist[M - 1];
-      double va[M];
-#pragma unroll
-      for (int k = 0; k < M; ++k) va[k] = (k < M - 1) ? hist[k] : ssum;
-      accum_dpp<NS, NU, M>(va, acc);  // row p-1
-    }
-    // note: the accumulation of row -1 at r = 0 adds products of zeros
+    va = __builtin_fma(smask, va, rd);
+    gacc_dpp<NUT, NU, M>(va, acc);  // row p-1
+    // (the accumulation at r = 0 adds products of the zero initial va)
 
-    // reduce over the ny rows through LDS; row 0 of lanes ns .. ns + nu_tot stores
+    // reduce over the ny rows through LDS; row 0 of the gather lanes stores
     if (red_lane) {
 #pragma unroll
-      for (int k = 0; k < NVM; ++k) red_w[k] = acc[k];
+      for (int k = 0; k < NV; ++k) red_w[k] = acc[k];
     }
-    if (row == 0 && col >= NS && col <= NS + nu_tot) {
-      double tot[NVM];
+    if (row == 0 && col < NG) {
+      double tot[NV];
 #pragma unroll
-      for (int k = 0; k < NVM; ++k) tot[k] = acc[k];
+      for (int k = 0; k < NV; ++k) tot[k] = acc[k];
 #pragma unroll
       for (int o = 1; o < NY; ++o) {
-        const double* rr = red + ((o - 1) * (nu_tot + 1) + c_in) * NVM;
+        const double* rr = red + ((o - 1) * NG + col) * NV;
 #pragma unroll
-        for (int k = 0; k < NVM; ++k) tot[k] += rr[k];
+        for (int k = 0; k < NV; ++k) tot[k] += rr[k];
       }
       double* out = P.qp + (size_t)q * P.qp_len;
-      const int c = c_in;
-      const int nuo = nu_tot - NU, nVo = M * nuo;
+      constexpr int nuo = NUT - NU, nVo = M * nuo;
       const double* uwt = uw_all + s * NU * NU;
-      if (c < NU) {
+      const int k2 = col / NUT, c2 = col - k2 * NUT;
+      if (col == M * NUT) {
 #pragma unroll
-        for (int a = 0; a < NV; ++a)
+        for (int a = 0; a < NV; ++a) out[NV * NV + a] = tot[a];  // f
+      } else if (c2 < NU) {
 #pragma unroll
-          for (int k = 0; k < M; ++k) {
-            const double rw = (a / NU == k) ? uwt[(a % NU) * NU + c] : 0.0;
-            out[a * NV + k * NU + c] = tot[a * M + k] + rw;
-          }
-      } else if (c < nu_tot) {
-#pragma unroll
-        for (int a = 0; a < NV; ++a)
-#pragma unroll
-          for (int k = 0; k < M; ++k) out[NV * NV + NV + a * nVo + k * nuo + (c - NU)] = tot[a * M + k];
+        for (int a = 0; a < NV; ++a) {  // H = Su' W Su + blkdiag_m(uwt)
+          const double rw = (a / NU == k2) ? uwt[(a % NU) * NU + c2] : 0.0;
+          out[a * NV + k2 * NU + c2] = tot[a] + rw;
+        }
       } else {
 #pragma unroll
-        for (int a = 0; a < NV; ++a) out[NV * NV + a] = tot[a * M];
+        for (int a = 0; a < NV; ++a) out[NV * NV + NV + a * nVo + k2 * nuo + (c2 - NU)] = tot[a];  // G
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -475,16 +464,20 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
 // launchers — explicit instantiation list (cf. the reference's *_list.h)
 // ---------------------------------------------------------------------------
 #define BUILD_CASE(NS_, NY_, NU_, M_)                                                  \
-  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2) {                   \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {                   \
     const size_t lds = sizeof(double) * ((size_t)P.lds_block +                         \
                                          (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);  \
-    int per_cu = 1;                                                                    \
+    if (lds > 64 * 1024)                                                               \
+      (void)hipFuncSetAttribute(                                                       \
+          reinterpret_cast<const void*>(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>),   \
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
+    int per_cu = 0;                                                                    \
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
-            &per_cu, cmpc_build_kernel<NS_, NY_, NU_, M_, 2>, 64 * CMPC_BUILD_WAVES,  \
+            &per_cu, cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>, 64 * CMPC_BUILD_WAVES,  \
             lds) != hipSuccess || per_cu < 1)                                         \
-      per_cu = 1;                                                                      \
+      per_cu = std::max<int>(1, (int)((160 * 1024) / lds));                            \
     const int grid = std::max(1, std::min(P.grid, P.cus * per_cu));                   \
-    hipLaunchKernelGGL((cmpc_build_kernel<NS_, NY_, NU_, M_, 2>), dim3(grid),           \
+    hipLaunchKernelGGL((cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>), dim3(grid),           \
                        dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                        \
     return 0;                                                                          \
   }
