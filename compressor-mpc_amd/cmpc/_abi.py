@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcmpc.so")
+LIB_PATH = os.environ.get("CMPC_LIBRARY") or os.path.join(_HERE, "libcmpc.so")
 
 CMPC_MAX_INPUTS = 8
 CMPC_MAX_NV = 8

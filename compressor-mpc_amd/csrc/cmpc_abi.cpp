@@ -430,6 +430,72 @@ int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
   return 0;
 }
 
+// LDS layout of the build kernel (doubles; must match cmpc_kernels.hip).
+// Bank model (MI355X_MICROARCH.md §LDS): ds_read_b64 is serviced per 32-lane
+// group with 32 double-wide banks, ds_write_b64 per 16-lane group with 16.
+// Per step the gather lanes of rows 0/1 (one read group) read lines at
+// line_off[c] + (m-1-k) + r - D_c and row o's Markov lanes write at
+// line_off[c] + m - 1 + r.  Lines (length m - 1 + p) are placed so that input
+// c's read window sits at residues [m*pi(c), m*pi(c) + m) mod 32 and the
+// write residues are distinct mod 16; rows are 16 mod 32 apart so row 1's
+// window is disjoint from row 0's.  All addresses advance together, so a
+// layout that is conflict-free at one step is conflict-free at every step.
+static void build_lds_layout(const cmpc_dims& d, const cmpc_layout& L, BuildParams* P) {
+  const int nut = d.nu_tot, M = d.m, ng = M * nut + 1;
+  auto up = [](int v, int a) { return (v + a - 1) / a * a; };
+  auto place = [&](const int* perm, int* off) {  // returns total length
+    int cur = 0;
+    for (int c = 0; c < nut; ++c) {
+      const int want = (((M * perm[c] + d.delay[c]) % 32) + 32) % 32;
+      int o = cur;
+      while (((o % 32) + 32) % 32 != want) ++o;
+      off[c] = o;
+      cur = o + M - 1 + d.p;
+    }
+    return cur;
+  };
+  int perm[CMPC_MAX_INPUTS], best[CMPC_MAX_INPUTS], off[CMPC_MAX_INPUTS];
+  for (int c = 0; c < nut; ++c) perm[c] = best[c] = c;
+  int best_len = -1;
+  do {  // permutations of the read windows: first one whose writes are conflict-free
+    const int len = place(perm, off);
+    bool ok = true;
+    for (int a = 0; a < nut && ok; ++a)
+      for (int b = a + 1; b < nut && ok; ++b)
+        ok = (off[a] - off[b]) % 16 != 0;
+    if (ok && (best_len < 0 || len < best_len)) {
+      best_len = len;
+      for (int c = 0; c < nut; ++c) best[c] = perm[c];
+    }
+  } while (std::next_permutation(perm, perm + nut));
+  const int len = place(best, off);
+  for (int c = 0; c < nut; ++c) P->line_off[c] = off[c];
+  int rs = up(len, 2);
+  while (rs % 32 != 16) rs += 2;
+  P->line_rs = rs;
+  const int head = L.rec_len + 8 + d.ny * L.nobs + 4;  // record, u_old, C_hat, kappa
+  int o = std::max(std::max(d.ny * rs, (d.ny - 1) * ng * L.nV), head);
+  o = up(o, 32) + 16;                                   // w table at 16 mod 32
+  P->w_off = o;
+  o += up((d.p + 3) * d.ny, 2);
+  while (o % 32 != (M * nut) % 32) o += 2;               // z slots next to row 0's window
+  P->zs_off = o;
+  o += d.ny * 4;
+  P->lds_per_wave = up(o, 32);
+  P->yl_stride = up((d.p + 1) * d.ny, 32);
+  P->lds_block = up(d.S * P->yl_stride + d.S * d.ny * d.ny + d.S * d.nu * d.nu + 16, 32);
+  // loop segments: the distinct delays inside the horizon, ascending
+  P->nbound = 0;
+  for (int c = 0; c < nut; ++c) {
+    const int D = d.delay[c];
+    if (D <= 0 || D >= d.p) continue;
+    bool seen = false;
+    for (int i = 0; i < P->nbound; ++i) seen = seen || P->bound[i] == D;
+    if (!seen) P->bound[P->nbound++] = D;
+  }
+  std::sort(P->bound, P->bound + P->nbound);
+}
+
 int cmpc_build(cmpc_ctx* c) {
   if (!c) return fail("null context");
   if (ensure_cfg(c)) return -1;
@@ -469,19 +535,7 @@ int cmpc_build(cmpc_ctx* c) {
     }
   }
   P.dmax = dmax;
-  {
-    P.lds_block = d.S * (d.p + 1) * d.ny + d.S * d.ny * d.ny + d.S * d.nu * d.nu + 16;
-    P.lds_block = (P.lds_block + 1) / 2 * 2;
-    // must match the kernel's per-wave layout (cmpc_kernels.hip)
-    int rowlen = 0;
-    for (int c = 0; c < d.nu_tot; ++c) rowlen += d.delay[c] + d.m - 1 + d.p;
-    rowlen += rowlen & 1;
-    const int ng = d.m * d.nu_tot + 1;
-    const int head = L.rec_len + 8 + d.ny * L.nobs + 4;  // record, u_old, C_hat, kappa
-    const int lines = (std::max(std::max(d.ny * rowlen, (d.ny - 1) * ng * L.nV), head) + 1) / 2 * 2;
-    P.lds_per_wave = lines + ((d.p + 3) * d.ny + 1) / 2 * 2 + d.ny * 4 + 64 + 4;
-    P.lds_per_wave = (P.lds_per_wave + 1) / 2 * 2;  // 16-byte aligned wave regions
-  }
+  build_lds_layout(d, L, &P);
   if (L.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return fail("lin record too long for the build kernel");
   const size_t lds_bytes = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
   if (lds_bytes > 160 * 1024) return fail("horizon/delays too long for the build kernel's LDS");

@@ -32,8 +32,17 @@ struct BuildParams {
   int dinput[CMPC_ND_MAX];       // per delayed index: input c
   int dlen[CMPC_ND_MAX];         // per delayed index: delay D
   int boff[CMPC_ND_MAX];         // per delayed index: offset of its shift block in dx_aug
-  int lds_block;                 // doubles of block-shared LDS (yhat of all sub-controllers)
-  int lds_per_wave;              // doubles of per-wave LDS (record, w, ring)
+  // LDS layout (doubles), computed on the host by build_lds_layout() so that
+  // the per-step hand-off reads/writes are free of bank conflicts
+  int lds_block;                 // block-shared: yhat (S x yl_stride), lwt, uwt, zeros
+  int yl_stride;                 // per sub-controller yhat stride (multiple of 32)
+  int lds_per_wave;              // per-wave region (multiple of 32)
+  int line_off[CMPC_MAX_INPUTS]; // delay line of input c inside a row
+  int line_rs;                   // delay-line row stride (one row per output)
+  int w_off;                     // w table
+  int zs_off;                    // free-response hand-off slots (NY x 4)
+  int nbound;                    // distinct delays 0 < D < p, ascending (loop segments)
+  int bound[CMPC_MAX_INPUTS];
   int grid;                      // workgroups needed (one QP per wave); launcher caps it
   int cus;                       // compute units of the device
 };

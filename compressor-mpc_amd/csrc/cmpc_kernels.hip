@@ -29,11 +29,55 @@
 #include "cmpc_internal.h"
 #include "dpp_blocks.inc"
 
+// Ablation switches for timing experiments (tools/ablate.sh); the product
+// build uses CMPC_EXP = 0.
+#ifndef CMPC_EXP
+#define CMPC_EXP 0
+#endif
+#if CMPC_EXP == 1
+#define CMPC_EXP_GACC(v, acc) (void)0
+#else
+#define CMPC_EXP_GACC(v, acc) gacc_dpp<NUT, NU, M>(v, acc)
+#endif
+#if CMPC_EXP == 2
+#define CMPC_EXP_HAND(...) rd = a;
+#else
+#define CMPC_EXP_HAND(...) __VA_ARGS__
+#endif
+#if CMPC_EXP == 3
+#define CMPC_EXP_PROP(pv, m, a) prop1_dpp<6>(pv, m, a)
+#else
+#define CMPC_EXP_PROP(pv, m, a) prop1w_dpp<NS, ND>(pv, m, a)
+#endif
+#if CMPC_EXP == 4
+#define CMPC_EXP_YH(...) yh = yh * 0.5
+#else
+#define CMPC_EXP_YH(...) __VA_ARGS__
+#endif
+#if CMPC_EXP == 5
+#define CMPC_EXP_STEP(pv, m, a, va, acc)                  \
+  {                                                       \
+    double a1_ = 0.0;                                     \
+    prop2w_dpp<NS, ND>(pv, m, a, a1_);                    \
+    a = a + a1_;                                          \
+    CMPC_EXP_GACC(va, acc);                               \
+  }
+#elif CMPC_EXP == 6
+#define CMPC_EXP_STEP(pv, m, a, va, acc) prop1w_gacc_dpp<NS, ND, NUT, NU, M>(pv, m, a, va, acc)
+#else
+#define CMPC_EXP_STEP(pv, m, a, va, acc) \
+  {                                      \
+    CMPC_EXP_PROP(pv, m, a);             \
+    CMPC_EXP_GACC(va, acc);              \
+  }
+#endif
+
 // ---------------------------------------------------------------------------
 // build kernel
 // ---------------------------------------------------------------------------
 template <int NS, int NY, int NUT, int NU, int M, int ND>
-__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(BuildParams P) {
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void cmpc_build_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
   constexpr int NG = M * NUT + 1;  // gather lanes per row: QP columns (move k, input c), then z
@@ -54,39 +98,48 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
   // D_c + M - 1 entries are zero (history before t = 0), raw Markov value of
   // step r at index D_c + M - 1 + r.  Reading index (M - 1 - k) + r yields the
   // column (move k, input c) of row r for every c: the delay shifts out.
-  int coff[NUT], rowlen = 0;
+  // (offsets chosen on the host for conflict-free banking: build_lds_layout)
+  int coff[NUT];
 #pragma unroll
-  for (int c = 0; c < NUT; ++c) {
-    coff[c] = rowlen;
-    rowlen += P.delay[c] + M - 1 + pp;
-  }
-  rowlen += rowlen & 1;  // 16-byte aligned rows
+  for (int c = 0; c < NUT; ++c) coff[c] = P.line_off[c];
+  const int rowlen = P.line_rs;
 
   // ---- LDS layout (doubles) ----
-  // block: [yhat S x (p+1) x NY][lwt S x NY x NY][uwt S x NU x NU][zeros 16]
+  // block: [yhat S x yl_stride][lwt S x NY x NY][uwt S x NU x NU][zeros 16]
   // wave : [rec rec_len][uold 8][chat NY x nobs][kappa 4]   (prologue only)
   //        overlaid by [delay lines NY x rowlen] (horizon loop), then by the
   //        row reduction (epilogue); followed by
   //        [w (p+3) x NY][z slots NY x U][scratch 64 + U]
   double* yl_all = smem;
-  double* lw_all = yl_all + S * (pp + 1) * NY;
+  double* lw_all = yl_all + S * P.yl_stride;
   double* uw_all = lw_all + S * NY * NY;
   double* zeros = uw_all + S * NU * NU;
   double* recl = smem + P.lds_block + wave * P.lds_per_wave;
   const int o_uold = rec_len, o_chat = o_uold + 8, o_kap = o_chat + NY * nobs;
-  const int o_line = 0;
-  const int o_w = (max(max(NY * rowlen, (NY - 1) * NG * NV), o_kap + 4) + 1) / 2 * 2;
-  const int o_zl = o_w + ((pp + 3) * NY + 1) / 2 * 2;
+  const int o_line = 0, o_w = P.w_off, o_zl = P.zs_off;
+  // Delay parameters in registers (compile-time indices only): a runtime-
+  // indexed read of the kernel-argument struct inside the QP loop would be a
+  // global load whose vmcnt(0) wait also drains the record prefetch.
+  int wdl[NDW], wbo[NDW], wdi[NDW];
+#pragma unroll
+  for (int k = 0; k < NDW; ++k) {
+    wdl[k] = (k < ND) ? P.dlen[k] : 0;
+    wbo[k] = (k < ND) ? P.boff[k] : 0;
+    wdi[k] = (k < ND) ? P.dinput[k] : 0;
+  }
+  const int nbound = P.nbound;
+  int bnd[NUT];
+#pragma unroll
+  for (int c = 0; c < NUT; ++c) bnd[c] = P.bound[c];
   double* uol = recl + o_uold;
   double* chat = recl + o_chat;
   double* kap = recl + o_kap;
   double* wl = recl + o_w;
   double* lines = recl + o_line;
   double* zl = recl + o_zl;
-  double* scratch = zl + NY * U;  // write target of lanes without a hand-off role
   double* red = lines;
-  for (int e = threadIdx.x; e < S * (pp + 1) * NY; e += 64 * CMPC_BUILD_WAVES) {
-    const int ss = e / ((pp + 1) * NY), t = e - ss * (pp + 1) * NY;
+  for (int e = threadIdx.x; e < S * P.yl_stride; e += 64 * CMPC_BUILD_WAVES) {
+    const int ss = e / P.yl_stride, t = e - ss * P.yl_stride;
     yl_all[e] = (t < pp * NY) ? P.cfg[(size_t)ss * P.co.len + P.co.yhat + t] : 0.0;
   }
   for (int e = threadIdx.x; e < S * NY * NY; e += 64 * CMPC_BUILD_WAVES)
@@ -125,21 +178,38 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
   // hand-off: writers store their chain value of step r, gather lanes read
   // the QP column values of row r (one masked LDS write + read per step)
   // (delay-line pointers advance one entry per step, z slots are reused)
-  double* wp = scratch + lane;
+  double* wp = zl;  // (masked: lanes without a writer role do not store)
   int winc = 0, rinc = 0;
-  if (mlane) { wp = lines + row * rowlen + coff[c_in] + P.delay[c_in] + M - 1; winc = 1; }
+  if (mlane) { wp = lines + row * rowlen + coff[c_in] + M - 1; winc = 1; }
   else if (slane) wp = zl + oz * U;
+  // Gather lane (k, c) reads line c at (m-1-k) + r - D_c once r >= D_c and the
+  // zero slot before (the delay-line history); the loop is split at the
+  // distinct delays.  Lanes without a gather role read the zero slot too (a
+  // broadcast).
   const double* rp = zero_p;
+  const double* rline = zero_p;  // line pointer taken at r = gdel
+  int gdel = 0x7fffffff;
   double smask = 0.0;  // 1: running-sum column (move M-1)
   if (glane) {
     if (col < M * NUT) {
       const int k = col / NUT, c = col - k * NUT;
-      rp = lines + row * rowlen + coff[c] + (M - 1 - k);
+      rline = lines + row * rowlen + coff[c] + (M - 1 - k);
+      gdel = P.delay[c];
       smask = (k == M - 1) ? 1.0 : 0.0;
-      rinc = 1;
+      if (gdel == 0) { rp = rline; rinc = 1; }
     } else {
       rp = zl + row * U;
     }
+  }
+  // one history entry of one delay line per lane (first m-1 entries of each)
+  const bool zero_lane = M > 1 && lane < NY * NUT * (M - 1);
+  int zero_at = 0;
+  if (zero_lane) {
+    const int o = lane / (NUT * (M - 1)), rem = lane - o * NUT * (M - 1);
+    const int c = rem / (M > 1 ? M - 1 : 1), i = rem - c * (M > 1 ? M - 1 : 1);
+#pragma unroll
+    for (int cc = 0; cc < NUT; ++cc)
+      if (cc == c) zero_at = o * rowlen + coff[cc] + i;
   }
   const bool red_lane = (row >= 1 && row < NY) && col < NG;
   double* red_w = red + ((row >= 1 ? row - 1 : 0) * NG + col) * NV;
@@ -158,7 +228,7 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
 
   for (; q < P.nqp; q += nwaves) {
     const int s = q % S;
-    const double* yl = yl_all + s * (pp + 1) * NY;
+    const double* yl = yl_all + s * P.yl_stride;
     const double* lwt = lw_all + s * NY * NY;
     // record -> LDS, then issue the next record's loads
 #pragma unroll
@@ -193,9 +263,13 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
     for (int e = lane; e < (pp + 3) * NY; e += 64) {
       const int t = e / NY, k = e - t * NY;
       double v = 0.0;
-      if (k < ND && t < P.dlen[k]) {
-        const double x = (t == 0) ? xa[P.ndist + k] : xa[P.boff[k] + t - 1];
-        v = x - uol[P.dinput[k]];
+      int dl = 0, bo = 0, di = 0;
+#pragma unroll
+      for (int kk = 0; kk < ND; ++kk)
+        if (k == kk) { dl = wdl[kk]; bo = wbo[kk]; di = wdi[kk]; }
+      if (t < dl) {
+        const double x = (t == 0) ? xa[P.ndist + k] : xa[bo + t - 1];
+        v = x - uol[di];
       }
       wl[e] = v;
     }
@@ -222,11 +296,10 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
 #pragma unroll
     for (int k = 0; k < ND; ++k) pv += m[NS + k] * wl[k];  // sim: x_1 = f + Adelay w_0
 
-    // zero the delay lines (their first D_c + M - 1 entries are the history
-    // before t = 0; the rest is overwritten by the loop); the record area
-    // they overlay is dead once the operands above are in registers
-    for (int e = lane; e < (NY * rowlen + 1) / 2; e += 64)
-      reinterpret_cast<double2*>(lines)[e] = make_double2(0.0, 0.0);
+    // zero the first m-1 entries of every delay line (history before t = 0);
+    // the record area the lines overlay is dead once the operands above are
+    // in registers
+    if (zero_lane) lines[zero_at] = 0.0;
     double acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
@@ -243,32 +316,41 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) void cmpc_build_kernel(Build
   {                                                                                    \
     /* chain init: f (states), kappa - yhat_r (outputs), w_{r+2} (carriers) */         \
     double a = __builtin_fma(-ym, yh, base);                                           \
-    prop1w_dpp<NS, ND>(pv, m, a);                                                      \
     /* accumulate row r-1: acc[a] += column_a * own column (gather lanes) */          \
     va = __builtin_fma(smask, va, rd);                                                 \
-    gacc_dpp<NUT, NU, M>(va, acc);                                                     \
-    yh = ylp[(u) * NY];                                                                \
+    CMPC_EXP_STEP(pv, m, a, va, acc);                                                  \
+    CMPC_EXP_YH(yh = ylp[(u) * NY]);                                                   \
     /* a: P rows -> P_{r+1} / raw Markov of step r; sim lanes -> x_{r+2} / z_r */      \
     pv = a;                                                                            \
-    wq[u] = a;                                                                         \
-    rd = rq[u];                                                                        \
+    CMPC_EXP_HAND(if (mlane || slane) wq[u] = a; rd = rq[u];)                          \
   }
 
     int r = 0;
-    for (; r + U <= pp; r += U) {
-      CMPC_BUILD_STEP(0)
-      CMPC_BUILD_STEP(1)
-      CMPC_BUILD_STEP(2)
-      CMPC_BUILD_STEP(3)
-      wq += U * winc;
-      rq += U * rinc;
-      ylp += U * NY;
-    }
-    for (; r < pp; ++r) {
-      CMPC_BUILD_STEP(0)
-      wq += winc;
-      rq += rinc;
-      ylp += NY;
+    int rinc_q = rinc;
+    for (int seg = 0; seg <= nbound; ++seg) {
+      int r_end = pp;
+#pragma unroll
+      for (int c = 0; c < NUT; ++c)
+        if (c == seg && seg < nbound) r_end = bnd[c];
+      for (; r + U <= r_end; r += U) {
+        CMPC_BUILD_STEP(0)
+        CMPC_BUILD_STEP(1)
+        CMPC_BUILD_STEP(2)
+        CMPC_BUILD_STEP(3)
+        wq += U * winc;
+        rq += U * rinc_q;
+        ylp += U * NY;
+      }
+      for (; r < r_end; ++r) {
+        CMPC_BUILD_STEP(0)
+        wq += winc;
+        rq += rinc_q;
+        ylp += NY;
+      }
+      if (gdel == r) {  // delayed input's history is over: start reading its line
+        rq = rline;
+        rinc_q = 1;
+      }
     }
 #undef CMPC_BUILD_STEP
     va = __builtin_fma(smask, va, rd);

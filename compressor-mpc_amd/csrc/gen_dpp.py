@@ -60,6 +60,48 @@ def prop1w(ns, nd):
             f"  asm({body}\n      : \"+v\"(a)\n      : {ins});\n}}\n")
 
 
+def prop1w_gacc(ns, nd, nut, nu, mm):
+    """prop1w chain on a with the nu*mm gather FMAs (acc[a] += bcast(v)*v)
+    interleaved after the first chain links (independent work in the
+    dependent chain's latency shadow)."""
+    nv = nu * mm
+    # operands: %0 a, %1..%nv acc, then p, v, m[0..ns+nd-1]
+    P_, V_ = 1 + nv, 2 + nv
+    M0 = 3 + nv
+    chain = [f'"v_fmac_f64_dpp %0, %{P_}, %{M0 + l} row_newbcast:{l} {CTRL}\\n\\t"' for l in range(ns)]
+    chain += [f'"v_fmac_f64_dpp %0, %{P_}, %{M0 + ns + k} row_newbcast:{16 - nd + k} {CTRL}\\n\\t"'
+              for k in range(nd)]
+    g = [f'"v_fmac_f64_dpp %{1 + a}, %{V_}, %{V_} row_newbcast:{(a // nu) * nut + a % nu} {CTRL}\\n\\t"'
+         for a in range(nv)]
+    lines = ['"s_nop 1\\n\\t"']
+    gi = 0
+    for i, c in enumerate(chain):
+        lines.append(c)
+        if gi < len(g) and i % 2 == 0:
+            lines.append(g[gi]); gi += 1
+    lines += g[gi:]
+    outs = ", ".join(['"+v"(a)'] + [f'"+v"(acc[{a}])' for a in range(nv)])
+    ins = ", ".join(['"v"(p)', '"v"(v)'] + [f'"v"(m[{l}])' for l in range(ns + nd)])
+    body = "\n      ".join(lines)
+    return (f"template <> __device__ __forceinline__ void prop1w_gacc_dpp<{ns}, {nd}, {nut}, {nu}, {mm}>("
+            f"double p, const double* m, double& a, double v, double* acc) {{\n"
+            f"  asm({body}\n      : {outs}\n      : {ins});\n}}\n")
+
+
+def prop2w(ns, nd):
+    """two accumulator chains (a0 even links, a1 odd links)"""
+    links = [(l, f"{l}") for l in range(ns)] + [(ns + k, f"{16 - nd + k}") for k in range(nd)]
+    lines = ['"s_nop 1\\n\\t"']
+    for i, (mi, lane) in enumerate(links):
+        acc = "%0" if i % 2 == 0 else "%1"
+        lines.append(f'"v_fmac_f64_dpp {acc}, %2, %{3 + mi} row_newbcast:{lane} {CTRL}\\n\\t"')
+    ins = ", ".join(['"v"(p)'] + [f'"v"(m[{l}])' for l in range(ns + nd)])
+    body = "\n      ".join(lines)
+    return (f"template <> __device__ __forceinline__ void prop2w_dpp<{ns}, {nd}>(double p, const double* m,"
+            f" double& a0, double& a1) {{\n"
+            f"  asm({body}\n      : \"+v\"(a0), \"+v\"(a1)\n      : {ins});\n}}\n")
+
+
 def accum(lb, nu, mm):
     """acc is double[NU*M][M] flattened as acc[a*M + k]."""
     nv = nu * mm
@@ -119,13 +161,18 @@ def main():
              "template <int NUT, int NU, int M> __device__ __forceinline__ void gacc_dpp(double,"
              " double*);\n",
              "template <int NS, int ND> __device__ __forceinline__ void prop1w_dpp(double, const double*,"
-             " double&);\n"]
+             " double&);\n",
+             "template <int NS, int ND> __device__ __forceinline__ void prop2w_dpp(double, const double*,"
+             " double&, double&);\n",
+             "template <int NS, int ND, int NUT, int NU, int M> __device__ __forceinline__ void "
+             "prop1w_gacc_dpp(double, const double*, double&, double, double*);\n"]
     for ns in range(2, 16):
         parts.append(prop(ns))
         parts.append(prop1(ns))
         for nd in (1, 2, 3, 4):
             if ns + nd <= 16:
                 parts.append(prop1w(ns, nd))
+                parts.append(prop2w(ns, nd))
     # LB = NS (first Markov lane): the instantiated plants have NS = 10, 11
     for lb in (10, 11):
         for nu in (1, 2, 4):
@@ -136,6 +183,10 @@ def main():
             for mm in (1, 2, 3):
                 if mm * nut + 1 <= 16 and nu * mm <= 8:
                     parts.append(gacc(nut, nu, mm))
+    # fused chain + gather accumulation for the instantiated build kernels
+    for ns, nd, nut, nu, mm in [(11, 2, 4, 2, 2), (11, 2, 4, 4, 2), (10, 2, 4, 2, 2),
+                                (11, 2, 4, 2, 1), (11, 2, 4, 2, 3)]:
+        parts.append(prop1w_gacc(ns, nd, nut, nu, mm))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)

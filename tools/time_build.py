@@ -7,7 +7,8 @@ import cmpc
 from cmpc.configs import reference_setup
 from cmpc.synthetic import synthetic_batch
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-for p in (2, 10, 25, 50, 100):
+PS = [int(a) for a in sys.argv[2:]] or [2, 10, 25, 50, 100]
+for p in PS:
     cfg = cmpc.reference_config("par", "coop", p=p)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
