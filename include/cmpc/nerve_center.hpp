@@ -1,0 +1,339 @@
+// nerve_center.hpp — C++ host adapter over the C ABI (include/cmpc.h) that
+// keeps the reference's controller API, so a harness written against
+// katie-jones/compressor-mpc's NerveCenter / DistributedController changes its
+// type names, not its call pattern.  Header-only, C++17, no Eigen: vectors
+// are plain `const double*` (matrices row-major).
+//
+// Reference interface mirrored (paths relative to the reference root):
+//   ControllerInterface<System>::GetNextInput(y)      include/controller_interface.h:46
+//   NerveCenter ctor (controllers, n_solver_iterations) include/nerve_center.h:89-95
+//   NerveCenter::Initialize(x, u, u_full, y, dx)      include/nerve_center.h:98-104
+//   NerveCenter::SetWeights(uwt, ywt)                 include/nerve_center.h:107-110
+//   NerveCenter::SetWeights(uwt, {ywt_s})             include/nerve_center.h:113-116
+//   NerveCenter::SetOutputReference(y_ref)            include/nerve_center.h:119-122
+//   NerveCenter::GetNextInputWithTiming(y, n, t)      include/nerve_center.h:134-182
+//   InputConstraints<nu> (per sub-controller ctor arg) include/input_constraints.h:12-26
+//   read_files.h setup-file reader                    include/read_files.h:13-81
+//
+// One difference of substance: the reference's GetNextInput runs each
+// sub-controller's observer (Observer::ObserveAPosteriori, observer.cc:6-40)
+// before linearising.  The observer gain lives in the reference's missing
+// harness include (common-simulation.inc) and the observer is outside this
+// path, so GetNextInput takes the state estimate (x_hat and
+// the augmented-state tail) from the caller.  Everything from the
+// linearisation onwards — AugmentedLinearizedSystem::Update, condensation, QP
+// build, K Jacobi iterations, UpdateUOld/SendUHelper — runs here: the
+// linearisation on the host (cmpc_plant_lin_record), the rest on the GPU.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../cmpc.h"
+
+namespace cmpc {
+
+class Error : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+inline void Check(int rc, const char* what) {
+  if (rc != 0) {
+    const char* m = cmpc_last_error();
+    throw Error(std::string(what) + ": " + (m ? m : "error"));
+  }
+}
+
+enum class PlantType { Parallel = CMPC_PLANT_PARALLEL, Serial = CMPC_PLANT_SERIAL };
+enum class ControllerType { Centralized, Cooperative, NonCooperative };
+
+// The reference's compile-time controller configuration, as run-time values
+// (include/parallel_compressors_constants.h:68-94,
+//  include/serial_compressors_constants.h:82-110, include/common-variables.h).
+struct ControllerSpec {
+  PlantType plant = PlantType::Parallel;
+  ControllerType type = ControllerType::Cooperative;
+  int ns = 0, n_inputs = 0, n_outputs = 0, nu_tot = 0;  // plant
+  int nu = 0, ny = 0, ndist = 4, p = 100, m = 2;        // per sub-controller
+  std::vector<int> delays;                              // Delays, plant control-input order
+  std::vector<std::vector<int>> input_order;            // ControlInputIndices per sub-controller
+  std::vector<std::vector<int>> out_idx;                // ControlledOutputIndices per sub-controller
+  std::vector<int> plant_input_index;                   // ControlInputIndex (GetPlantInput)
+
+  int S() const { return static_cast<int>(input_order.size()); }
+  int nV() const { return m * nu; }
+
+  static ControllerSpec Reference(PlantType plant, ControllerType type, int p = 100, int m = 2) {
+    ControllerSpec c;
+    c.plant = plant;
+    c.type = type;
+    c.p = p;
+    c.m = m;
+    int nci = 0;
+    Check(cmpc_plant_dims(static_cast<int>(plant), &c.ns, &c.n_inputs, &c.n_outputs, &nci),
+          "cmpc_plant_dims");
+    c.nu_tot = nci;
+    c.delays = {0, 40, 0, 40};                 // ConstexprArray<0, 40, 0, 40>
+    c.plant_input_index = {0, 3, 4, 7};        // ConstexprArray<0, 3, 4, 7>
+    const std::vector<int> ci1{0, 1, 2, 3}, ci2{2, 3, 0, 1};  // ControlInputIndices1/2
+    std::vector<int> ctrl_out;
+    std::vector<std::vector<int>> nc_out;
+    if (plant == PlantType::Parallel) {
+      ctrl_out = {0, 1, 3};
+      nc_out = {{0, 3}, {1, 3}};
+    } else {
+      ctrl_out = {0, 1, 2, 3};
+      nc_out = {{0, 1}, {2, 3}};
+    }
+    switch (type) {
+      case ControllerType::Centralized:
+        c.nu = 4;
+        c.input_order = {ci1};
+        c.out_idx = {ctrl_out};
+        break;
+      case ControllerType::Cooperative:
+        c.nu = 2;
+        c.input_order = {ci1, ci2};
+        c.out_idx = {ctrl_out, ctrl_out};
+        break;
+      case ControllerType::NonCooperative:
+        c.nu = 2;
+        c.input_order = {ci1, ci2};
+        c.out_idx = nc_out;
+        break;
+    }
+    c.ny = static_cast<int>(c.out_idx[0].size());
+    return c;
+  }
+};
+
+// Setup file of the reference (setup/setup-<ctrl>-<plant>), read like
+// include/read_files.h:13-81: a key line, then whitespace-separated values.
+struct SetupFile {
+  int n_iterations = 1, n_timing_iterations = 1;
+  std::vector<double> yref, uwt, ywt, lower, upper, rate_lower, rate_upper;
+
+  static SetupFile Read(const std::string& path) {
+    std::ifstream in(path);
+    if (!in) throw Error("cannot open setup file " + path);
+    static const char* keys[] = {"n-iterations", "n-timing-iterations", "folder-name",
+                                 "output-filename", "yref", "uwt", "ywt",
+                                 "constraints-lower", "constraints-upper",
+                                 "constraints-rate-lower", "constraints-rate-upper",
+                                 "simulation"};
+    SetupFile s;
+    std::string line, key;
+    std::vector<double>* dst = nullptr;
+    std::vector<double> scratch;
+    while (std::getline(in, line)) {
+      std::istringstream ls(line);
+      std::string tok;
+      if (!(ls >> tok)) continue;
+      bool is_key = false;
+      for (const char* k : keys) is_key = is_key || tok == k;
+      if (is_key) {
+        key = tok;
+        dst = key == "yref" ? &s.yref : key == "uwt" ? &s.uwt : key == "ywt" ? &s.ywt
+            : key == "constraints-lower" ? &s.lower : key == "constraints-upper" ? &s.upper
+            : key == "constraints-rate-lower" ? &s.rate_lower
+            : key == "constraints-rate-upper" ? &s.rate_upper : &scratch;
+        continue;
+      }
+      if (key.empty()) throw Error("Error reading setup file at line: " + line);
+      if (key == "folder-name" || key == "output-filename") continue;
+      std::istringstream vs(line);
+      double v;
+      std::vector<double> vals;
+      while (vs >> v) vals.push_back(v);
+      if (key == "n-iterations" && !vals.empty()) s.n_iterations = static_cast<int>(vals[0]);
+      if (key == "n-timing-iterations" && !vals.empty())
+        s.n_timing_iterations = static_cast<int>(vals[0]);
+      dst->insert(dst->end(), vals.begin(), vals.end());
+    }
+    return s;
+  }
+};
+
+// NerveCenter<System, n_total_states, SubControllers...> for one plant
+// (B = 1, as the reference); `handle()` exposes the context for the batched
+// entry points of include/cmpc.h.
+class NerveCenter {
+ public:
+  NerveCenter(const ControllerSpec& spec, int n_solver_iterations, int device = 0)
+      : spec_(spec), K_(n_solver_iterations) {
+    d_ = cmpc_dims{};
+    d_.ns = spec.ns;
+    d_.ndist = spec.ndist;
+    d_.nu_tot = spec.nu_tot;
+    d_.nu = spec.nu;
+    d_.ny = spec.ny;
+    d_.p = spec.p;
+    d_.m = spec.m;
+    d_.S = spec.S();
+    d_.B = 1;
+    // delays in each sub-controller's input order; the ABI shares them
+    for (int c = 0; c < spec.nu_tot; ++c) {
+      d_.delay[c] = spec.delays[spec.input_order[0][c]];
+      for (int s = 1; s < spec.S(); ++s)
+        if (spec.delays[spec.input_order[s][c]] != d_.delay[c])
+          throw Error("sub-controllers with different delay orderings");
+    }
+    Check(cmpc_create(&ctx_, &d_, device), "cmpc_create");
+    Check(cmpc_get_layout(ctx_, &L_), "cmpc_get_layout");
+    u_old_.assign(spec.nu_tot, 0.0);
+    u_offset_.assign(spec.n_inputs, 0.0);
+    rec_.assign(static_cast<size_t>(spec.S()) * L_.rec_len, 0.0);
+  }
+  ~NerveCenter() {
+    if (ctx_) cmpc_destroy(ctx_);
+  }
+  NerveCenter(const NerveCenter&) = delete;
+  NerveCenter& operator=(const NerveCenter&) = delete;
+
+  cmpc_ctx* handle() { return ctx_; }
+  const ControllerSpec& spec() const { return spec_; }
+
+  /// SetWeights(uwt, ywt): uwt n_control_inputs^2, ywt n_outputs^2 (row-major);
+  /// each sub-controller takes uwt[own, own] and ywt[controlled, controlled].
+  void SetWeights(const double* uwt, const double* ywt) {
+    std::vector<const double*> per(spec_.S(), nullptr);
+    std::vector<std::vector<double>> tmp(spec_.S());
+    for (int s = 0; s < spec_.S(); ++s) {
+      tmp[s].resize(spec_.ny * spec_.ny);
+      for (int a = 0; a < spec_.ny; ++a)
+        for (int b = 0; b < spec_.ny; ++b)
+          tmp[s][a * spec_.ny + b] =
+              ywt[spec_.out_idx[s][a] * spec_.n_outputs + spec_.out_idx[s][b]];
+      per[s] = tmp[s].data();
+    }
+    SetWeights(uwt, per);
+  }
+  /// SetWeights(uwt, {ywt_s}): one ny x ny output weight per sub-controller.
+  void SetWeights(const double* uwt, const std::vector<const double*>& ywt_sub) {
+    for (int s = 0; s < spec_.S(); ++s) {
+      std::vector<double> u(spec_.nu * spec_.nu);
+      for (int a = 0; a < spec_.nu; ++a)
+        for (int b = 0; b < spec_.nu; ++b)
+          u[a * spec_.nu + b] =
+              uwt[spec_.input_order[s][a] * spec_.nu_tot + spec_.input_order[s][b]];
+      Check(cmpc_set_weights(ctx_, s, u.data(), ywt_sub[s]), "cmpc_set_weights");
+    }
+  }
+  /// SetOutputReference: y_ref is p_max x n_outputs (prediction-major).
+  void SetOutputReference(const double* y_ref) {
+    for (int s = 0; s < spec_.S(); ++s) {
+      std::vector<double> r(spec_.p * spec_.ny);
+      for (int i = 0; i < spec_.p; ++i)
+        for (int o = 0; o < spec_.ny; ++o)
+          r[i * spec_.ny + o] = y_ref[i * spec_.n_outputs + spec_.out_idx[s][o]];
+      Check(cmpc_set_reference(ctx_, s, r.data()), "cmpc_set_reference");
+    }
+  }
+  /// InputConstraints<nu> of sub-controller s (the reference passes them to
+  /// each DistributedController's constructor).
+  void SetConstraints(int s, const double* lower, const double* upper, const double* rate_lower,
+                      const double* rate_upper) {
+    Check(cmpc_set_constraints(ctx_, s, lower, upper, rate_lower, rate_upper),
+          "cmpc_set_constraints");
+  }
+
+  /// Initialize(x_init, u_init, u_init_full, y_init, dx_init): linearise at
+  /// (x_init, u_init_full), build every sub-controller's QP and run the cold
+  /// InitializeQPProblem solve (its working sets warm-start step 0).
+  void Initialize(const double* x_init, const double* u_init, const double* u_init_full,
+                  const double* y_init, const double* dx_init = nullptr) {
+    u_offset_.assign(u_init_full, u_init_full + spec_.n_inputs);
+    u_old_.assign(u_init, u_init + spec_.nu_tot);
+    std::vector<double> u_sub(static_cast<size_t>(spec_.S()) * spec_.nu_tot);
+    for (int s = 0; s < spec_.S(); ++s)
+      for (int c = 0; c < spec_.nu_tot; ++c)
+        u_sub[s * spec_.nu_tot + c] = u_init[spec_.input_order[s][c]];
+    std::vector<double> du(static_cast<size_t>(spec_.S()) * spec_.nV(), 0.0);
+    std::vector<uint32_t> ws(spec_.S(), 0u);
+    Check(cmpc_set_state(ctx_, u_sub.data(), du.data(), ws.data()), "cmpc_set_state");
+    FillRecords(x_init, u_init_full, dx_init, y_init);
+    Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
+    Check(cmpc_build(ctx_), "cmpc_build");
+    Check(cmpc_init_warmstart(ctx_), "cmpc_init_warmstart");
+    Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
+  }
+
+  /// ControllerInterface::GetNextInput with the observer's estimate supplied.
+  std::vector<double> GetNextInput(const double* y, const double* x_hat,
+                                   const double* dx_aug = nullptr) {
+    return GetNextInputWithTiming(y, x_hat, dx_aug);
+  }
+
+  /// GetNextInputWithTiming: if 0 <= n_timing_iterations < K, the wall time of
+  /// QP generation + the first n_timing_iterations Jacobi iterations is
+  /// returned in *time_out_ns (as the reference's cpu_timer); otherwise the
+  /// whole step is timed.
+  std::vector<double> GetNextInputWithTiming(const double* y, const double* x_hat,
+                                             const double* dx_aug = nullptr,
+                                             int n_timing_iterations = -1,
+                                             int64_t* time_out_ns = nullptr) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> u_full(u_offset_);
+    for (int c = 0; c < spec_.nu_tot; ++c) u_full[spec_.plant_input_index[c]] += u_old_[c];
+    FillRecords(x_hat, u_full.data(), dx_aug, y);
+    Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
+    Check(cmpc_build(ctx_), "cmpc_build");
+    int64_t timed = -1;
+    if (n_timing_iterations >= 0 && n_timing_iterations < K_) {
+      Check(cmpc_iterate(ctx_, n_timing_iterations, 0u), "cmpc_iterate");
+      Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
+      timed = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                  std::chrono::steady_clock::now() - t0).count();
+      Check(cmpc_iterate(ctx_, K_ - n_timing_iterations, CMPC_APPLY_MOVE), "cmpc_iterate");
+    } else {
+      Check(cmpc_iterate(ctx_, K_, CMPC_APPLY_MOVE), "cmpc_iterate");
+    }
+    du_.resize(static_cast<size_t>(spec_.S()) * spec_.nV());
+    status_.resize(spec_.S());
+    nwsr_.resize(spec_.S());
+    Check(cmpc_download(ctx_, du_.data(), status_.data(), nwsr_.data()), "cmpc_download");
+    // UpdateUOld (include/nerve_center.h:313-319): apply each first move
+    for (int s = 0; s < spec_.S(); ++s)
+      for (int c = 0; c < spec_.nu; ++c) u_old_[spec_.input_order[s][c]] += du_[s * spec_.nV() + c];
+    if (time_out_ns)
+      *time_out_ns = timed >= 0 ? timed
+                                : std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                      std::chrono::steady_clock::now() - t0).count();
+    return u_old_;
+  }
+
+  /// Move plans (S x nV), QP status words and working-set change counts of the last step.
+  const std::vector<double>& last_plans() const { return du_; }
+  const std::vector<int32_t>& last_status() const { return status_; }
+  const std::vector<int32_t>& last_nwsr() const { return nwsr_; }
+
+ private:
+  // AugmentedLinearizedSystem::Update + observer state tail + y_prev for every
+  // sub-controller (the inputs GenerateInitialQP reads).
+  void FillRecords(const double* x, const double* u_full, const double* dx_aug, const double* y) {
+    for (int s = 0; s < spec_.S(); ++s) {
+      double* r = rec_.data() + static_cast<size_t>(s) * L_.rec_len;
+      Check(cmpc_plant_lin_record(static_cast<int>(spec_.plant), 1.0, 1.0, 0.05, x, u_full,
+                                  spec_.input_order[s].data(), spec_.out_idx[s].data(), &d_, r),
+            "cmpc_plant_lin_record");
+      for (int i = 0; i < L_.naug; ++i) r[L_.off_x + i] = dx_aug ? dx_aug[i] : 0.0;
+      for (int o = 0; o < spec_.ny; ++o) r[L_.off_y + o] = y[spec_.out_idx[s][o]];
+    }
+  }
+
+  ControllerSpec spec_;
+  int K_;
+  cmpc_dims d_{};
+  cmpc_layout L_{};
+  cmpc_ctx* ctx_ = nullptr;
+  std::vector<double> u_old_, u_offset_, rec_, du_;
+  std::vector<int32_t> status_, nwsr_;
+};
+
+}  // namespace cmpc

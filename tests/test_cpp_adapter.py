@@ -1,0 +1,92 @@
+"""The C++ adapter (include/cmpc/nerve_center.hpp) — the reference's NerveCenter
+API over the C ABI — driven like the reference's tests/*-with-timing.cc
+harnesses: a setup file in the reference's format, SetWeights /
+SetOutputReference / constraints, Initialize, GetNextInputWithTiming.
+
+CPU: the driver builds and fails loudly (no CPU fallback) without a device.
+GPU: u(t = 0) matches the reference's own step-0 records (6 digits).
+"""
+import os
+import subprocess
+
+import pytest
+
+import golden_cases as GC
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DRIVER = os.path.join(HERE, "cpp", "nerve_center_step0")
+
+
+def _build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "cpp"), "nerve_center_step0"])
+    assert os.path.exists(DRIVER)
+
+
+def _mat(vals, n):
+    return "\n".join("\t".join("%g" % v for v in vals[r * n:(r + 1) * n]) for r in range(n))
+
+
+def write_setup(path, g, ny, S):
+    """setup/setup-<ctrl>-<plant> layout (key line, values, blank line)."""
+    nci = int(round(len(g["uwt"]) ** 0.5))
+    blk = ny * ny
+    yw = g["ywt"]
+    blocks = [yw[i * blk:(i + 1) * blk] for i in range(len(yw) // blk)]
+    parts = [
+        ("n-iterations", str(g["n_iterations"])),
+        ("n-timing-iterations", str(g["n_iterations"])),
+        ("folder-name", "parallel"),
+        ("output-filename", "out.dat"),
+        ("yref", " ".join("%g" % v for v in g["yref"])),
+        ("uwt", _mat(g["uwt"], nci)),
+        ("ywt", "\n\n".join(_mat(b, ny) for b in blocks)),
+        ("constraints-lower", "\t".join("%g" % v for v in g["constraints_lower"])),
+        ("constraints-upper", "\t".join("%g" % v for v in g["constraints_upper"])),
+        ("constraints-rate-lower", "\t".join("%g" % v for v in g["rate_lower"])),
+        ("constraints-rate-upper", "\t".join("%g" % v for v in g["rate_upper"])),
+    ]
+    with open(path, "w") as fh:
+        for k, v in parts:
+            fh.write(f"{k}\n{v}\n\n")
+
+
+def test_driver_builds_and_fails_loudly_without_device(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    _build()
+    cfg, _, _, g = GC.case("coop-par")
+    setup = tmp_path / "setup-coop-par"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([DRIVER, str(setup), "par", "coop"], capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "error: cmpc_create" in r.stderr
+
+
+def test_setup_writer_roundtrip(tmp_path):
+    """The written file parses back (Python mirror of read_files.h) to the fixture."""
+    from cmpc.configs import SetupFile
+    cfg, setup, _, g = GC.case("coop-par")
+    path = tmp_path / "s"
+    write_setup(path, g, cfg.ny, cfg.S)
+    back = SetupFile.parse(path.read_text(), cfg)
+    assert back.n_iterations == g["n_iterations"]
+    assert back.uwt == g["uwt"]
+    assert back.ywt[0] == setup.ywt[0] and back.ywt[1] == setup.ywt[1]
+    assert back.rate_upper == g["rate_upper"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "ncoop-ser"])
+def test_gpu_cpp_adapter_step0_matches_reference(name, tmp_path):
+    _build()
+    cfg, _, _, g = GC.case(name)
+    ctype, plant = name.split("-")
+    setup = tmp_path / f"setup-{name}"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([DRIVER, str(setup), plant, ctype], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    u = [float(t) for t in r.stdout.split()]
+    assert "status: " + " ".join(["0"] * cfg.S) in r.stderr, r.stderr
+    GC.assert_six_digits(u, g["u0"])
