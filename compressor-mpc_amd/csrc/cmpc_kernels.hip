@@ -400,7 +400,8 @@ void cmpc_build_kernel(BuildParams P) {
 // Jacobi iterate kernel (lane per QP)
 // ---------------------------------------------------------------------------
 template <int N, int NU, int NVO>
-__global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_solve_kernel(SolveParams P) {
+__global__ __launch_bounds__(CMPC_SOLVE_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void cmpc_solve_kernel(SolveParams P) {
   constexpr int M = N / NU;
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
@@ -413,7 +414,10 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_solve_kernel(SolvePar
   const double* rec = P.qp + (size_t)q * P.qp_len;
   const double* cfg = P.cfg + (size_t)s * P.co.len;
 
-  double H[N][N], f[N], G[N][NVOA];
+  // G = Su' W Su_other is read once per Jacobi iteration: it lives in LDS
+  // (transposed, lane-contiguous) rather than in 2*N*NVO registers
+  __shared__ double gsh[N * NVOA][CMPC_SOLVE_THREADS];
+  double H[N][N], f[N];
 #pragma unroll
   for (int a = 0; a < N; ++a)
 #pragma unroll
@@ -423,21 +427,20 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_solve_kernel(SolvePar
 #pragma unroll
   for (int a = 0; a < N; ++a)
 #pragma unroll
-    for (int c = 0; c < NVOA; ++c) G[a][c] = (NVO > 0) ? rec[N * N + N + a * NVO + c] : 0.0;
+    for (int c = 0; c < NVOA; ++c)
+      gsh[a * NVOA + c][threadIdx.x] = (NVO > 0) ? rec[N * N + N + a * NVO + c] : 0.0;
 
-  Qp<N, NU> qp;
+  Qp<N, NU, NU> qp;  // bounds repeat every NU entries: rep_m(lower - u_old), rep_m(rate)
   double uo[NU];
 #pragma unroll
   for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
 #pragma unroll
-  for (int mv = 0; mv < M; ++mv)
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      qp.lb[mv * NU + c] = cfg[P.co.lower + c] - uo[c];
-      qp.ub[mv * NU + c] = cfg[P.co.upper + c] - uo[c];
-      qp.lbA[mv * NU + c] = cfg[P.co.rlower + c];
-      qp.ubA[mv * NU + c] = cfg[P.co.rupper + c];
-    }
+  for (int c = 0; c < NU; ++c) {
+    qp.lb[c] = cfg[P.co.lower + c] - uo[c];
+    qp.ub[c] = cfg[P.co.upper + c] - uo[c];
+    qp.lbA[c] = cfg[P.co.rlower + c];
+    qp.ubA[c] = cfg[P.co.rupper + c];
+  }
   const bool pd = hinv_of<N>(H, qp.Hinv);
   double hmax = 0.0;
 #pragma unroll
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_solve_kernel(SolvePar
       for (int a = 0; a < N; ++a) {
         double t = fk[a];
 #pragma unroll
-        for (int c = 0; c < NVOA; ++c) t = t + G[a][c] * dother[c];
+        for (int c = 0; c < NVOA; ++c) t = t + gsh[a * NVOA + c][threadIdx.x] * dother[c];
         fk[a] = t;
       }
     }

@@ -32,11 +32,18 @@ CMPC_HD double sel(const double (&v)[N], int i) {
   return r;
 }
 
-template <int N, int NU>
+// NB = stored bound entries: N (general), or NU when the bounds repeat every
+// NU entries (the MPC QP: rep_m(lower - u_old), rep_m(rate bounds),
+// libs/mpc_qp_solver.cc:53-60), which halves their registers.
+template <int N, int NU, int NB = N>
 struct Qp {
+  static_assert(NB == N || NB == NU, "bounds: general or NU-periodic");
   double Hinv[N][N];
-  double lb[N], ub[N], lbA[N], ubA[N];
+  double lb[NB], ub[NB], lbA[NB], ubA[NB];
+  CMPC_HD double lbv(int j) const { return sel<NB>(lb, j % NB); }
+  CMPC_HD double ubv(int j) const { return sel<NB>(ub, j % NB); }
 
+  // nu_{j,side}' v for a compile-time j (the phase-B scan; sel folds away)
   CMPC_HD double nu_dot(int j, int side, const double (&v)[N]) const {
     double t;
     if (j < N) {
@@ -47,30 +54,53 @@ struct Qp {
     }
     return side ? -t : t;
   }
-  CMPC_HD void hinv_nu(int j, int side, double (&out)[N]) const {
+  CMPC_HD double beta(int j, int side) const {
+    if (j < N) return side ? -sel<NB>(ub, j % NB) : sel<NB>(lb, j % NB);
+    return side ? -sel<NB>(ubA, (j - N) % NB) : sel<NB>(lbA, (j - N) % NB);
+  }
+  // Normal of constraint (j, side) as an explicit vector (entries 0, +-1):
+  // bound j < N: +-e_j; rate row i = j - N: +-(e_i - e_{i-NU}) for i >= NU,
+  // +-e_i otherwise.  Products with it are exact, and every sum below has at
+  // most two nonzero terms accumulated in ascending column order, so ndot /
+  // hinv_n round exactly like the oracle's nu_dot / hinv_nu
+  // (round(v_i - v_{i-NU}), negated for the upper side).
+  CMPC_HD void normal(int j, int side, double (&n)[N]) const {
+    const double sg = side ? -1.0 : 1.0;
+    const bool rate = j >= N;
+    const int i = rate ? j - N : j;
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+      n[c] = (c == i) ? sg : ((rate && i >= NU && c == i - NU) ? -sg : 0.0);
+  }
+  // out = Hinv n
+  CMPC_HD void hinv_n(const double (&n)[N], double (&out)[N]) const {
 #pragma unroll
     for (int r = 0; r < N; ++r) {
-      double t;
-      if (j < N) {
-        t = sel<N>(Hinv[r], j);
-      } else {
-        const int i = j - N;
-        t = (i >= NU) ? sel<N>(Hinv[r], i) - sel<N>(Hinv[r], i - NU) : sel<N>(Hinv[r], i);
-      }
-      out[r] = side ? -t : t;
+      double t = 0.0;
+#pragma unroll
+      for (int c = 0; c < N; ++c) t = fma(Hinv[r][c], n[c], t);
+      out[r] = t;
     }
-  }
-  CMPC_HD double beta(int j, int side) const {
-    if (j < N) return side ? -sel<N>(ub, j) : sel<N>(lb, j);
-    return side ? -sel<N>(ubA, j - N) : sel<N>(lbA, j - N);
   }
 };
 
+// n' v (n an explicit constraint normal; exact as noted at Qp::normal)
+template <int N>
+CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
+  double t = 0.0;
+#pragma unroll
+  for (int c = 0; c < N; ++c) t = fma(n[c], v[c], t);
+  return t;
+}
+
+// Working set: slots 0..K-1 sorted by constraint index j, each with its
+// normal, bound beta, multiplier and h = Hinv * normal.
 template <int N>
 struct WSet {
   int K;
   int j[N], side[N];
   double lam[N];
+  double nrm[N][N], bta[N];
   double h[N][N];
   double L[N][N], D[N];
 };
@@ -131,18 +161,19 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
   }
 }
 
-template <int N, int NU>
-CMPC_HD bool wset_factor(const Qp<N, NU>& q, WSet<N>& W) {
+// (re)build h, M = N' Hinv N and its LDL' for the current working set
+template <int N, int NU, int NB>
+CMPC_HD bool wset_factor(const Qp<N, NU, NB>& q, WSet<N>& W) {
   double M[N][N];
 #pragma unroll
   for (int a = 0; a < N; ++a)
-    if (a < W.K) q.hinv_nu(W.j[a], W.side[a], W.h[a]);
+    if (a < W.K) q.hinv_n(W.nrm[a], W.h[a]);
 #pragma unroll
   for (int a = 0; a < N; ++a)
 #pragma unroll
     for (int b = a; b < N; ++b) {
       double v = 0.0;
-      if (b < W.K) v = q.nu_dot(W.j[a], W.side[a], W.h[b]);
+      if (b < W.K) v = ndot<N>(W.nrm[a], W.h[b]);
       M[a][b] = v;
       M[b][a] = v;
     }
@@ -157,12 +188,16 @@ CMPC_HD void wset_drop(WSet<N>& W, int a) {
       W.j[b] = W.j[b + 1];
       W.side[b] = W.side[b + 1];
       W.lam[b] = W.lam[b + 1];
+      W.bta[b] = W.bta[b + 1];
+#pragma unroll
+      for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b + 1][c];
     }
   W.K--;
 }
 
+// sorted insert (phase B adds; the warm start fills slots directly)
 template <int N>
-CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam) {
+CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam, const double (&n)[N], double bta) {
   int pos = 0;
 #pragma unroll
   for (int b = 0; b < N; ++b)
@@ -173,6 +208,9 @@ CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam) {
       W.j[b] = W.j[b - 1];
       W.side[b] = W.side[b - 1];
       W.lam[b] = W.lam[b - 1];
+      W.bta[b] = W.bta[b - 1];
+#pragma unroll
+      for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b - 1][c];
     }
 #pragma unroll
   for (int b = 0; b < N; ++b)
@@ -180,6 +218,9 @@ CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam) {
       W.j[b] = j;
       W.side[b] = side;
       W.lam[b] = lam;
+      W.bta[b] = bta;
+#pragma unroll
+      for (int c = 0; c < N; ++c) W.nrm[b][c] = n[c];
     }
   W.K++;
 }
@@ -222,8 +263,8 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], double (&Hinv)[N][N]) {
   return true;
 }
 
-template <int N, int NU>
-CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&g)[N],
+template <int N, int NU, int NB>
+CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const double (&g)[N],
                          uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
   WSet<N> W;
   o.status = CMPC_QP_OK;
@@ -251,15 +292,27 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
     for (int j = 0; j < N; ++j) sacc = sacc + q.Hinv[i][j] * g[j];
     xu[i] = -sacc;
   }
-  // A. warm start
-  if (!done) {
+  // A. warm start: slot a = the a-th active constraint of ws_in in ascending
+  // j (the oracle adds them in that order while K < n)
+  {
+    uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
 #pragma unroll
-    for (int j = 0; j < 2 * N; ++j)
-      if ((ws_in >> j) & 1u)
-        if (W.K < N) wset_add<N>(W, j, (ws_in >> (16 + j)) & 1u, 0.0);
+    for (int a = 0; a < N; ++a) {
+      if (msk) {
+        const int j = __builtin_ctz(msk);
+        msk &= msk - 1u;
+        const int sd = (ws_in >> (16 + j)) & 1u;
+        W.j[a] = j;
+        W.side[a] = sd;
+        W.lam[a] = 0.0;
+        q.normal(j, sd, W.nrm[a]);
+        W.bta[a] = q.beta(j, sd);
+        W.K = a + 1;
+      }
+    }
   }
   for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
-    if (!wset_factor<N, NU>(q, W)) {
+    if (!wset_factor<N, NU, NB>(q, W)) {
       W.K = 0;
       ++chg;
       continue;
@@ -267,7 +320,7 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
     double rhs[N];
 #pragma unroll
     for (int a = 0; a < N; ++a)
-      rhs[a] = (a < W.K) ? q.beta(W.j[a], W.side[a]) - q.nu_dot(W.j[a], W.side[a], xu) : 0.0;
+      rhs[a] = (a < W.K) ? W.bta[a] - ndot<N>(W.nrm[a], xu) : 0.0;
     ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
     int worst = -1;
     double wv = -tol_d;
@@ -326,12 +379,15 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
       }
     }
     if (pj < 0) break;  // optimal
+    double np_[N];
+    q.normal(pj, ps, np_);
+    const double bp = q.beta(pj, ps);
     double up = 0.0;
     for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
       double hp[N], qv[N], rv[N], z[N];
-      q.hinv_nu(pj, ps, hp);
+      q.hinv_n(np_, hp);
 #pragma unroll
-      for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? q.nu_dot(W.j[a], W.side[a], hp) : 0.0;
+      for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? ndot<N>(W.nrm[a], hp) : 0.0;
       ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
 #pragma unroll
       for (int r = 0; r < N; ++r) {
@@ -341,8 +397,8 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
           if (a < W.K) v = v - rv[a] * W.h[a][r];
         z[r] = v;
       }
-      const double zn = q.nu_dot(pj, ps, z);
-      const double den = q.nu_dot(pj, ps, hp);
+      const double zn = ndot<N>(np_, z);
+      const double den = ndot<N>(np_, hp);
       int k = -1;
       double t1 = 0.0;
 #pragma unroll
@@ -378,10 +434,10 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
           done = true;
           break;
         }
-        wset_factor<N, NU>(q, W);
+        wset_factor<N, NU, NB>(q, W);
         continue;
       }
-      const double sl = q.nu_dot(pj, ps, x) - q.beta(pj, ps);
+      const double sl = ndot<N>(np_, x) - bp;
       const double t2 = -sl / zn;
       const bool full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
@@ -393,13 +449,13 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
       up = up + t;
       if (full) {
         trace_push(o, 1, pj, ps);
-        wset_add<N>(W, pj, ps, up);
+        wset_add<N>(W, pj, ps, up, np_, bp);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
           done = true;
           break;
         }
-        wset_factor<N, NU>(q, W);
+        wset_factor<N, NU, NB>(q, W);
         break;
       }
       int kj = 0, ks = 0;
@@ -416,7 +472,7 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
         done = true;
         break;
       }
-      wset_factor<N, NU>(q, W);
+      wset_factor<N, NU, NB>(q, W);
     }
   }
   o.nchg = chg;
@@ -432,7 +488,7 @@ CMPC_HD void qp_solve(const Qp<N, NU>& q, bool pd, double tol_d, const double (&
       if (a < W.K && W.j[a] < N) {
 #pragma unroll
         for (int r = 0; r < N; ++r)
-          if (r == W.j[a]) x[r] = W.side[a] ? q.ub[r] : q.lb[r];
+          if (r == W.j[a]) x[r] = W.side[a] ? q.ubv(r) : q.lbv(r);
       }
   } else {
 #pragma unroll

@@ -1,0 +1,78 @@
+"""The product's QP solver (compressor-mpc_amd/csrc/qp_solver.h), compiled for
+the host (tests/cpp/libqp_host.so), against the oracle's solver
+(oracle/or_qp.c, the specification of DESIGN.md §4): bit-exact x, status,
+number of working-set changes, final working set and change sequence, on
+random MPC-shaped QPs with random warm starts.  The GPU suite checks the same
+code on the device (test_gpu_parity.py)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "libqp_host.so")
+
+
+def host():
+    if not os.path.exists(LIB):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(LIB), "libqp_host.so"])
+    lib = ctypes.CDLL(LIB)
+    lib.qp_host_solve.restype = ctypes.c_int
+    return lib
+
+
+def d(a):
+    return np.ascontiguousarray(a, np.float64).ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def host_solve(lib, H, g, lb, ub, lbA, ubA, nu, ws_in, max_chg=10):
+    n = len(g)
+    x = np.zeros(n)
+    st = ctypes.c_int32(); nchg = ctypes.c_int32(); ws = ctypes.c_uint32(); ntr = ctypes.c_int32()
+    tr = (ctypes.c_uint8 * 16)()
+    rc = lib.qp_host_solve(n, nu, d(H), d(g), d(lb), d(ub), d(lbA), d(ubA), ctypes.c_uint32(ws_in),
+                           max_chg, x.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                           ctypes.byref(st), ctypes.byref(nchg), ctypes.byref(ws), tr,
+                           ctypes.byref(ntr))
+    assert rc == 0
+    return x, st.value, nchg.value, ws.value, bytes(tr)[:ntr.value]
+
+
+def random_qp(rng, n, nu):
+    """MPC-like: SPD H with the move-blocked coupling, box + rate limits."""
+    A = rng.normal(size=(n, n))
+    H = A @ A.T + n * np.diag(rng.uniform(0.5, 3.0, n))
+    H = 0.5 * (H + H.T)
+    g = rng.normal(0, 3.0, n) * rng.choice([0.1, 1.0, 10.0])
+    m = n // nu
+    lo = rng.uniform(-0.5, 0.0, nu); hi = lo + rng.uniform(0.05, 1.0, nu)
+    rlo = -rng.uniform(0.02, 0.3, nu); rhi = rng.uniform(0.02, 0.3, nu)
+    return (H, g, np.tile(lo, m), np.tile(hi, m), np.tile(rlo, m), np.tile(rhi, m))
+
+
+@pytest.mark.parametrize("n,nu", [(4, 2), (8, 4)])
+def test_host_solver_bitexact_vs_oracle(n, nu):
+    lib = host()
+    rng = np.random.default_rng(2024 + n)
+    stats = {}
+    for trial in range(3000):
+        H, g, lb, ub, lbA, ubA = random_qp(rng, n, nu)
+        ws_in = 0
+        if trial % 3:
+            for j in rng.choice(2 * n, size=rng.integers(0, n + 1), replace=False):
+                ws_in |= (1 << int(j)) | ((int(rng.integers(0, 2)) << (16 + int(j))))
+        max_chg = 10 if trial % 7 else int(rng.integers(0, 4))
+        xh, st, nchg, ws, tr = host_solve(lib, H, g, lb, ub, lbA, ubA, nu, ws_in, max_chg)
+        xo, info = O.qp_solve(H, g, lb, ub, lbA, ubA, nu, ws_in, max_chg=max_chg)
+        assert st == info.status, trial
+        assert nchg == info.nchg, trial
+        assert ws == info.ws, trial
+        assert tr == bytes(info.trace[:info.ntrace]), trial
+        assert np.array_equal(xh, xo), (trial, xh, xo)
+        stats[st] = stats.get(st, 0) + 1
+        stats["active"] = stats.get("active", 0) + (ws != 0)
+    # the sample exercises the constrained paths
+    assert stats["active"] > 1000 and stats.get(0, 0) > 1000
