@@ -250,3 +250,40 @@ def test_gpu_large_batch_properties():
                           np.zeros(len(qs), np.uint32), init=True)
     np.testing.assert_allclose(du.reshape(B, 2, n)[sample].reshape(-1, n), odu, rtol=1e-9,
                                atol=1e-10)
+
+
+# SURVEY.md §8(d) configs restated as parity cases (the bench line is config
+# "coop p=50"; these run at their own sizes): (2) coop-par p=20 B=4096 K=9,
+# (3) ncoop-par p=50 B=65536 K=1, (5) cent-par p=200 B=1024 K=1.
+SURVEY_CONFIGS = [("par", "coop", 20, 4096, 9), ("par", "ncoop", 50, 65536, 1),
+                  ("par", "cent", 200, 1024, 1)]
+
+
+@pytest.mark.parametrize("plant,ctype,p,B,K", SURVEY_CONFIGS)
+def test_gpu_survey_config(plant, ctype, p, B, K):
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arr = cmpc.controller_arrays(cfg, setup)
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=300 + p, n_distinct=min(B, 1024))
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.build()
+        H, f, G = ctx.download_qp()
+        ctx.init_warmstart()
+        ctx.iterate(K)
+        du, st, _ = ctx.download()
+    assert (st == 0).mean() > 0.999
+    assert np.all(H == np.transpose(H, (0, 2, 1)))
+    # a sample of whole scenarios against the oracle: QP data and plans
+    S, n = cfg.S, cfg.nV
+    sample = np.arange(0, B, max(1, B // 24))
+    qs = (sample[:, None] * S + np.arange(S)[None, :]).reshape(-1)
+    lin_s, u_s = np.ascontiguousarray(lin[qs]), np.ascontiguousarray(u_old[qs])
+    Ho, fo, Go = oracle_qps(cfg, arr, lin_s, u_s)
+    for i, q in enumerate(qs):
+        sH = np.abs(Ho[i]).max()
+        np.testing.assert_allclose(H[q], Ho[i], rtol=0, atol=1e-11 * sH)
+        np.testing.assert_allclose(f[q], fo[i], rtol=0, atol=1e-10 * max(np.abs(fo[i]).max(), 1e-6 * sH))
+    sub = CmpcDims.from_config(cfg, len(sample))
+    odu, ost, *_ = O.step(sub, arr, lin_s, K, u_s.copy(), np.zeros((len(qs), n)),
+                          np.zeros(len(qs), np.uint32), init=True)
+    np.testing.assert_allclose(du[qs], odu, rtol=1e-9, atol=1e-10)
