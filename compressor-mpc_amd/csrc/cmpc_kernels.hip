@@ -396,6 +396,14 @@ void cmpc_build_kernel(BuildParams P) {
 
 #include "qp_solver.h"
 
+// H^-1 of one lane as column `base` of a [N*N][T] lane-contiguous LDS array
+template <int N, int T>
+struct HinvLds {
+  double* base;
+  __device__ __forceinline__ double operator()(int r, int c) const { return base[(r * N + c) * T]; }
+  __device__ __forceinline__ void set(int r, int c, double v) { base[(r * N + c) * T] = v; }
+};
+
 // ---------------------------------------------------------------------------
 // Jacobi iterate kernel (lane per QP)
 // ---------------------------------------------------------------------------
@@ -430,7 +438,10 @@ void cmpc_solve_kernel(SolveParams P) {
     for (int c = 0; c < NVOA; ++c)
       gsh[a * NVOA + c][threadIdx.x] = (NVO > 0) ? rec[N * N + N + a * NVO + c] : 0.0;
 
-  Qp<N, NU, NU> qp;  // bounds repeat every NU entries: rep_m(lower - u_old), rep_m(rate)
+  // bounds repeat every NU entries (rep_m(lower - u_old), rep_m(rate bounds));
+  // H^-1 stays in registers (an LDS copy measured slower: the compiler
+  // hoists its loads and spills more)
+  Qp<N, NU, NU> qp;
   double uo[NU];
 #pragma unroll
   for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];

@@ -32,13 +32,22 @@ CMPC_HD double sel(const double (&v)[N], int i) {
   return r;
 }
 
+// Storage of H^-1: registers (default) or a per-lane column of a
+// lane-contiguous LDS array (the solve kernel, to keep 2 waves/SIMD).
+template <int N>
+struct HinvRegs {
+  double m[N][N];
+  CMPC_HD double operator()(int r, int c) const { return m[r][c]; }
+  CMPC_HD void set(int r, int c, double v) { m[r][c] = v; }
+};
+
 // NB = stored bound entries: N (general), or NU when the bounds repeat every
 // NU entries (the MPC QP: rep_m(lower - u_old), rep_m(rate bounds),
 // libs/mpc_qp_solver.cc:53-60), which halves their registers.
-template <int N, int NU, int NB = N>
+template <int N, int NU, int NB = N, class HS = HinvRegs<N>>
 struct Qp {
   static_assert(NB == N || NB == NU, "bounds: general or NU-periodic");
-  double Hinv[N][N];
+  HS Hinv;
   double lb[NB], ub[NB], lbA[NB], ubA[NB];
   CMPC_HD double lbv(int j) const { return sel<NB>(lb, j % NB); }
   CMPC_HD double ubv(int j) const { return sel<NB>(ub, j % NB); }
@@ -78,7 +87,7 @@ struct Qp {
     for (int r = 0; r < N; ++r) {
       double t = 0.0;
 #pragma unroll
-      for (int c = 0; c < N; ++c) t = fma(Hinv[r][c], n[c], t);
+      for (int c = 0; c < N; ++c) t = fma(Hinv(r, c), n[c], t);
       out[r] = t;
     }
   }
@@ -162,8 +171,8 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
 }
 
 // (re)build h, M = N' Hinv N and its LDL' for the current working set
-template <int N, int NU, int NB>
-CMPC_HD bool wset_factor(const Qp<N, NU, NB>& q, WSet<N>& W) {
+template <int N, class Q>
+CMPC_HD bool wset_factor(const Q& q, WSet<N>& W) {
   double M[N][N];
 #pragma unroll
   for (int a = 0; a < N; ++a)
@@ -243,8 +252,8 @@ CMPC_HD void trace_push(QpOut& o, int add, int j, int side) {
 }
 
 // Hinv = H^-1 via LDL' (oracle/or_qp.c step 0).  Returns false if not PD.
-template <int N>
-CMPC_HD bool hinv_of(const double (&H)[N][N], double (&Hinv)[N][N]) {
+template <int N, class HS>
+CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
   double L[N][N], D[N];
   if (!ldl_k<N>(N, H, L, D)) return false;
 #pragma unroll
@@ -254,17 +263,17 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], double (&Hinv)[N][N]) {
     for (int i = 0; i < N; ++i) e[i] = (i == c) ? 1.0 : 0.0;
     ldl_solve_k<N>(N, L, D, e, colv);
 #pragma unroll
-    for (int i = 0; i <= c; ++i) Hinv[i][c] = colv[i];
+    for (int i = 0; i <= c; ++i) Hinv.set(i, c, colv[i]);
   }
 #pragma unroll
   for (int c = 0; c < N; ++c)
 #pragma unroll
-    for (int i = 0; i < c; ++i) Hinv[c][i] = Hinv[i][c];
+    for (int i = 0; i < c; ++i) Hinv.set(c, i, Hinv(i, c));
   return true;
 }
 
-template <int N, int NU, int NB>
-CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const double (&g)[N],
+template <int N, int NU, int NB, class HS>
+CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
                          uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
   WSet<N> W;
   o.status = CMPC_QP_OK;
@@ -289,7 +298,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const doubl
   for (int i = 0; i < N; ++i) {
     double sacc = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + q.Hinv[i][j] * g[j];
+    for (int j = 0; j < N; ++j) sacc = sacc + q.Hinv(i, j) * g[j];
     xu[i] = -sacc;
   }
   // A. warm start: slot a = the a-th active constraint of ws_in in ascending
@@ -312,7 +321,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const doubl
     }
   }
   for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
-    if (!wset_factor<N, NU, NB>(q, W)) {
+    if (!wset_factor<N>(q, W)) {
       W.K = 0;
       ++chg;
       continue;
@@ -434,7 +443,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const doubl
           done = true;
           break;
         }
-        wset_factor<N, NU, NB>(q, W);
+        wset_factor<N>(q, W);
         continue;
       }
       const double sl = ndot<N>(np_, x) - bp;
@@ -455,7 +464,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const doubl
           done = true;
           break;
         }
-        wset_factor<N, NU, NB>(q, W);
+        wset_factor<N>(q, W);
         break;
       }
       int kj = 0, ks = 0;
@@ -472,7 +481,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB>& q, bool pd, double tol_d, const doubl
         done = true;
         break;
       }
-      wset_factor<N, NU, NB>(q, W);
+      wset_factor<N>(q, W);
     }
   }
   o.nchg = chg;
