@@ -106,7 +106,7 @@ def main():
     ap.add_argument("--p", type=int, default=50)
     ap.add_argument("--K", type=int, default=9)
     ap.add_argument("--input-batches", type=int, default=4)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -219,7 +219,7 @@ def main():
         "roofline": {
             "bound": "mfma",
             "pipe": "fp64 VALU (v_fmac_f64_dpp); MI355X FP64 vector peak = FP64 matrix peak",
-            "kernel": "cmpc_build_kernel<11,3,2,2>",
+            "kernel": "cmpc_build_kernel<NS=11,NY=3,NUT=4,NU=2,M=2,ND=2>",
             "achieved": achieved_tf,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
