@@ -103,14 +103,14 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
 }
 
 // Working set: slots 0..K-1 sorted by constraint index j, each with its
-// normal, bound beta, multiplier and h = Hinv * normal.
+// normal, bound beta and multiplier.  h_a = Hinv * normal_a is recomputed
+// where it is used (registers: the solve kernel runs at 2 waves/SIMD).
 template <int N>
 struct WSet {
   int K;
   int j[N], side[N];
   double lam[N];
   double nrm[N][N], bta[N];
-  double h[N][N];
   double L[N][N], D[N];
 };
 
@@ -175,17 +175,17 @@ template <int N, class Q>
 CMPC_HD bool wset_factor(const Q& q, WSet<N>& W) {
   double M[N][N];
 #pragma unroll
-  for (int a = 0; a < N; ++a)
-    if (a < W.K) q.hinv_n(W.nrm[a], W.h[a]);
+  for (int b = 0; b < N; ++b) {
+    double hb[N];
+    if (b < W.K) q.hinv_n(W.nrm[b], hb);
 #pragma unroll
-  for (int a = 0; a < N; ++a)
-#pragma unroll
-    for (int b = a; b < N; ++b) {
+    for (int a = 0; a <= b; ++a) {
       double v = 0.0;
-      if (b < W.K) v = ndot<N>(W.nrm[a], W.h[b]);
+      if (b < W.K) v = ndot<N>(W.nrm[a], hb);
       M[a][b] = v;
       M[b][a] = v;
     }
+  }
   return ldl_k<N>(W.K, M, W.L, W.D);
 }
 
@@ -355,13 +355,17 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
     }
   }
   if (!done) {
+    // x = xu + sum_a lam_a h_a (per r, a ascending as the oracle)
 #pragma unroll
-    for (int r = 0; r < N; ++r) {
-      double v = xu[r];
+    for (int r = 0; r < N; ++r) x[r] = xu[r];
 #pragma unroll
-      for (int a = 0; a < N; ++a)
-        if (a < W.K) v = v + W.lam[a] * W.h[a][r];
-      x[r] = v;
+    for (int a = 0; a < N; ++a) {
+      if (a < W.K) {
+        double ha[N];
+        q.hinv_n(W.nrm[a], ha);
+#pragma unroll
+        for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
+      }
     }
   }
   // B. Goldfarb–Idnani
@@ -399,12 +403,15 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
       for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? ndot<N>(W.nrm[a], hp) : 0.0;
       ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
 #pragma unroll
-      for (int r = 0; r < N; ++r) {
-        double v = hp[r];
+      for (int r = 0; r < N; ++r) z[r] = hp[r];
 #pragma unroll
-        for (int a = 0; a < N; ++a)
-          if (a < W.K) v = v - rv[a] * W.h[a][r];
-        z[r] = v;
+      for (int a = 0; a < N; ++a) {
+        if (a < W.K) {
+          double ha[N];
+          q.hinv_n(W.nrm[a], ha);
+#pragma unroll
+          for (int r = 0; r < N; ++r) z[r] = z[r] - rv[a] * ha[r];
+        }
       }
       const double zn = ndot<N>(np_, z);
       const double den = ndot<N>(np_, hp);
