@@ -158,6 +158,24 @@ class Context:
         """Bind an external device-resident record array (0 = own buffer)."""
         check(self.lib.cmpc_bind_lin(self._h, ctypes.c_void_p(device_ptr or None)), "cmpc_bind_lin")
 
+    def produce_lin(self, x_ptr: int, u_full_ptr: int, y_ptr: int, dx_aug_ptr: int = 0,
+                    Ts: float = 0.05, p_in: float = 1.0, p_out: float = 1.0):
+        """Device producer (cmpc_produce_lin): linearise + discretise the plant
+        for every scenario on the GPU and write this context's lin records.
+        Arguments are device pointers (e.g. torch tensor .data_ptr())."""
+        io = np.ascontiguousarray(self.cfg.input_order, dtype=np.int32)
+        oi = np.ascontiguousarray(self.cfg.out_idx, dtype=np.int32)
+        check(self.lib.cmpc_produce_lin(
+            self._h, self.cfg.plant, p_in, p_out, Ts, iptr(io), iptr(oi), ctypes.c_void_p(x_ptr),
+            ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(dx_aug_ptr or None), ctypes.c_void_p(y_ptr)),
+            "cmpc_produce_lin")
+
+    def download_lin(self) -> np.ndarray:
+        """The context's own record buffer (B*S, rec_len), e.g. after produce_lin."""
+        out = np.zeros((self.B * self.cfg.S, self.layout.rec_len))
+        check(self.lib.cmpc_download_lin(self._h, dptr(out)), "cmpc_download_lin")
+        return out
+
     # -- hot path --------------------------------------------------------
     def build(self):
         check(self.lib.cmpc_build(self._h), "cmpc_build")

@@ -81,6 +81,7 @@ EXPORTS = (
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
+    "cmpc_produce_lin", "cmpc_download_lin",
 )
 
 _lib = None
@@ -114,6 +115,7 @@ def load_library(path: str = LIB_PATH):
         "cmpc_get_state": ([c_void, P(dbl), P(dbl), P(u32)], ctypes.c_int),
         "cmpc_upload_lin": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_lin_device": ([c_void], c_void),
+        "cmpc_download_lin": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_bind_lin": ([c_void, c_void], ctypes.c_int),
         "cmpc_build": ([c_void], ctypes.c_int),
         "cmpc_init_warmstart": ([c_void], ctypes.c_int),
@@ -131,6 +133,8 @@ def load_library(path: str = LIB_PATH):
         "cmpc_plant_output": ([ctypes.c_int, P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_plant_lin_record": ([ctypes.c_int, dbl, dbl, dbl, P(dbl), P(dbl), P(i32), P(i32),
                                    P(CmpcDims), P(dbl)], ctypes.c_int),
+        "cmpc_produce_lin": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), c_void, c_void,
+                              c_void, c_void], ctypes.c_int),
         "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),
                                  P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32), ctypes.c_int,
                                  P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],

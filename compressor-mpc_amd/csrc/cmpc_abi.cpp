@@ -416,6 +416,15 @@ int cmpc_upload_lin(cmpc_ctx* c, const double* lin) {
   return 0;
 }
 
+int cmpc_download_lin(cmpc_ctx* c, double* lin) {
+  if (!c || !lin) return fail("null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(lin, c->lin, sizeof(double) * (size_t)c->nqp * c->L.rec_len,
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 void* cmpc_lin_device(cmpc_ctx* c) { return c ? (void*)c->lin : nullptr; }
 
 int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
@@ -428,6 +437,56 @@ int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
   }
   c->lin_bound = lin_device;
   return 0;
+}
+
+int cmpc_produce_lin(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
+                     const int32_t* input_order, const int32_t* out_idx, const double* x,
+                     const double* u_full, const double* dx_aug, const double* y) {
+  if (!c) return fail("null context");
+  if (!input_order || !out_idx || !x || !u_full || !y) return fail("cmpc_produce_lin: null argument");
+  const cmpc_dims& d = c->d;
+  const cmpc_layout& L = c->L;
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(plant, &ns, &ni, &no, &nci)) return fail("cmpc_produce_lin: unknown plant");
+  if (d.ns != ns || d.nu_tot != nci || d.ndist > no || d.ny > 4)
+    return fail("cmpc_produce_lin: context dimensions do not match the plant");
+  if (d.S > CMPC_MAX_S_PRODUCE) return fail("cmpc_produce_lin: too many sub-controllers");
+  ProduceParams P;
+  std::memset(&P, 0, sizeof P);
+  P.lin = c->lin;
+  P.x = x;
+  P.u_full = u_full;
+  P.dx_aug = dx_aug;
+  P.y = y;
+  P.B = d.B;
+  P.S = d.S;
+  P.rec_len = L.rec_len;
+  P.nu_tot = d.nu_tot;
+  P.ny = d.ny;
+  P.nobs = L.nobs;
+  P.naug = L.naug;
+  P.n_outputs = no;
+  P.off_A = L.off_A; P.off_B = L.off_B; P.off_C = L.off_C;
+  P.off_f = L.off_f; P.off_x = L.off_x; P.off_y = L.off_y;
+  P.p_in = p_in;
+  P.p_out = p_out;
+  P.Ts = Ts;
+  for (int s = 0; s < d.S; ++s) {
+    for (int k = 0; k < d.nu_tot; ++k) {
+      const int v = input_order[s * d.nu_tot + k];
+      if (v < 0 || v >= nci) return fail("cmpc_produce_lin: bad input_order");
+      P.input_order[s][k] = v;
+    }
+    for (int o = 0; o < d.ny; ++o) {
+      const int v = out_idx[s * d.ny + o];
+      if (v < 0 || v >= no) return fail("cmpc_produce_lin: bad out_idx");
+      P.out_idx[s][o] = v;
+    }
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  c->lin_bound = nullptr;  // the build reads the produced records
+  if (cmpc_launch_produce(P, plant, c->stream)) return fail("cmpc_produce_lin: launch failed");
+  return check_launch("produce kernel");
 }
 
 // LDS layout of the build kernel (doubles; must match cmpc_kernels.hip).

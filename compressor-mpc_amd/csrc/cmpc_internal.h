@@ -75,9 +75,26 @@ struct QpBatchParams {
   int nqp, max_chg;
 };
 
-// Kernel launchers (cmpc_kernels.hip).  Return 0 or -1 (unsupported dims).
+// Device record producer (produce.hip): one scenario's plant linearisation
+// -> its S lin records.
+#define CMPC_MAX_S_PRODUCE 8
+struct ProduceParams {
+  double* lin;                  // B*S*rec_len, written
+  const double* x;              // B*ns
+  const double* u_full;         // B*n_inputs
+  const double* dx_aug;         // B*S*naug or null (zeros)
+  const double* y;              // B*n_outputs
+  int B, S, rec_len, nu_tot, ny, nobs, naug, n_outputs;
+  int off_A, off_B, off_C, off_f, off_x, off_y;
+  double p_in, p_out, Ts;
+  int input_order[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS];
+  int out_idx[CMPC_MAX_S_PRODUCE][4];
+};
+
+// Kernel launchers (cmpc_kernels.hip, produce.hip).  Return 0 or -1 (unsupported dims).
 int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
                       void* stream);
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
+int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream);

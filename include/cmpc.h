@@ -134,6 +134,9 @@ int cmpc_get_state(cmpc_ctx* ctx, double* u_old, double* du_old, uint32_t* ws);
  * written in place by a device-side producer through cmpc_lin_device(). */
 int cmpc_upload_lin(cmpc_ctx* ctx, const double* lin_host);
 void* cmpc_lin_device(cmpc_ctx* ctx);
+/* Copy the context's own record buffer to the host (B*S*rec_len doubles),
+ * e.g. to inspect what cmpc_produce_lin wrote. */
+int cmpc_download_lin(cmpc_ctx* ctx, double* lin_host);
 /* Bind an external device-resident record array (B*S*rec_len doubles on the
  * ctx device, e.g. the output of a device-side producer); NULL re-binds the
  * context's own buffer.  Takes effect for the next cmpc_build. */
@@ -190,6 +193,20 @@ int cmpc_plant_lin_record(int plant, double p_in, double p_out, double Ts,
                           const double* x, const double* u_full,
                           const int32_t* input_order, const int32_t* out_idx,
                           const cmpc_dims* dims, double* record);
+
+/* Device producer: AugmentedLinearizedSystem::Update
+ * (libs/aug_lin_sys.cc:145-177, DiscretizeRK4 :232-255) for every scenario b
+ * of the context's batch, on the GPU.  Linearises the plant at (x[b],
+ * u_full[b]), discretises with sampling time Ts and writes the S lin records
+ * of b into the context's own record buffer (replacing any cmpc_bind_lin
+ * binding): input columns in input_order[s] order (host, S x nu_tot),
+ * controlled rows out_idx[s] (host, S x ny), the observer tail dx_aug
+ * (B*S x naug, or NULL for zeros) and y_prev = y[b][out_idx[s]].
+ * x (B x ns), u_full (B x n_inputs), dx_aug and y (B x n_outputs) are DEVICE
+ * pointers; the call is asynchronous on the context's stream. */
+int cmpc_produce_lin(cmpc_ctx* ctx, int plant, double p_in, double p_out, double Ts,
+                     const int32_t* input_order, const int32_t* out_idx, const double* x,
+                     const double* u_full, const double* dx_aug, const double* y);
 
 #ifdef __cplusplus
 }
