@@ -20,6 +20,8 @@ namespace {
 
 using namespace cmpc_plant;
 
+// DiscretizeRK4 (libs/aug_lin_sys.cc:232-255).  Products accumulate with fma
+// in k order: the device producer's DPP chains (produce.hip) do the same.
 void discretize(int ns, double Ts, const double* A, const double* B, const double* f, double* Ad,
                 double* Bd, double* fd) {
   double A2[256], A3[256], Ac[256];
@@ -27,7 +29,7 @@ void discretize(int ns, double Ts, const double* A, const double* B, const doubl
     for (int i = 0; i < ns; ++i)
       for (int j = 0; j < ns; ++j) {
         double s = 0;
-        for (int k = 0; k < ns; ++k) s += X[i * ns + k] * Y[k * ns + j];
+        for (int k = 0; k < ns; ++k) s = std::fma(X[i * ns + k], Y[k * ns + j], s);
         Z[i * ns + j] = s;
       }
   };
@@ -43,11 +45,11 @@ void discretize(int ns, double Ts, const double* A, const double* B, const doubl
   for (int i = 0; i < ns; ++i) {
     for (int j = 0; j < 4; ++j) {
       double s = 0;
-      for (int k = 0; k < ns; ++k) s += Ac[i * ns + k] * B[k * 4 + j];
+      for (int k = 0; k < ns; ++k) s = std::fma(Ac[i * ns + k], B[k * 4 + j], s);
       Bd[i * 4 + j] = s;
     }
     double s = 0;
-    for (int k = 0; k < ns; ++k) s += Ac[i * ns + k] * f[k];
+    for (int k = 0; k < ns; ++k) s = std::fma(Ac[i * ns + k], f[k], s);
     fd[i] = s;
   }
 }

@@ -154,14 +154,18 @@ struct Compressor {
 };
 
 // Continuous linearisation of a reference plant: A ns x ns, B ns x 4, C 4 x ns, f ns.
+// zero_out = false: A, B, C are already zero (the device producer clears
+// them with the whole wave; one lane then writes only the nonzeros)
 CMPC_PHD void parallel_linearize(double p_in, double p_out, const double* x, const double* u, double* A,
-                        double* B, double* C, double* f) {
+                        double* B, double* C, double* f, bool zero_out = true) {
   const int ns = 11;
   Compressor comp{CompressorParams(), true};
   TankParams tank;
-  zero(A, ns * ns);
-  zero(B, ns * 4);
-  zero(C, 4 * ns);
+  if (zero_out) {
+    zero(A, ns * ns);
+    zero(B, ns * 4);
+    zero(C, 4 * ns);
+  }
   double cC[2][10], flow_total = 0;
   for (int i = 0; i < 2; ++i) {
     const double uc[6] = {u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3], p_in, x[10]};
@@ -199,12 +203,14 @@ CMPC_PHD void serial_derivative(double p_in, double p_out, const double* x, cons
 }
 
 CMPC_PHD void serial_linearize(double p_in, double p_out, const double* x, const double* u, double* A,
-                      double* B, double* C, double* f) {
+                      double* B, double* C, double* f, bool zero_out = true) {
   const int ns = 10;
   Compressor first{CompressorParams(), true}, follower{CompressorParams(), false};
-  zero(A, ns * ns);
-  zero(B, ns * 4);
-  zero(C, 4 * ns);
+  if (zero_out) {
+    zero(A, ns * ns);
+    zero(B, ns * 4);
+    zero(C, 4 * ns);
+  }
   double cA[25], cB[10], cC[10], cf[5], mo;
   const double u0[6] = {u[0], u[1], u[2], u[3], p_in, x[5]};
   first.linearize(x, u0, cA, cB, cC, cf, &mo);

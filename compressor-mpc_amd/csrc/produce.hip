@@ -7,15 +7,17 @@
 //   record assembly            cmpc_plant_lin_record (plant.cpp) + the
 //                              observer tail dx_aug and the controlled y
 //
-// One wave per scenario.  Lane 0 runs the scalar plant model into LDS; the
-// 11x11 products of the discretisation are spread over the 64 lanes with the
-// host's summation order (k ascending, separate multiply and add), and the S
-// records of the scenario are written with lane-contiguous stores.
+// Four scenarios per wave, one per 16-lane DPP row.  Lane 0 of each row runs
+// the scalar plant model into LDS (the four side by side); the 11x11 products
+// of the discretisation are DPP broadcast-FMA chains (v_fmac_f64_dpp
+// row_newbcast, as the build kernel), and the S records of the scenario are
+// written through a per-workgroup element -> source table.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "cmpc_internal.h"
 #include "plant_model.h"
+#include "dpp_blocks.inc"
 
 namespace {
 
@@ -27,98 +29,130 @@ namespace {
     __builtin_amdgcn_wave_barrier();                          \
   } while (0)
 
-constexpr int kWaves = 4;          // waves (scenarios) per workgroup
+constexpr int kWaves = 4;          // waves per workgroup
+constexpr int kSpw = 4;            // scenarios per wave: one per 16-lane row
+constexpr int kLanes = 64 / kSpw;  // lanes per scenario
 constexpr int kMat = 121;          // ns x ns, ns <= 11
-constexpr int kWaveLds = 8 * kMat + 4 * 11 * 2 + 11 * 2 + 32;  // doubles per wave
+// per scenario: A, Ad, Bc, Bd, Cc, fc, fd, x, u
+constexpr int kScnLds = 2 * kMat + 4 * 44 + 2 * 11 + 2 * 11 + 3;
 
-// Z = X Y (n x n), entries spread over the wave: the host's mm order
-__device__ __forceinline__ void mm_wave(int n, int lane, const double* X, const double* Y,
-                                        double* Z) {
-  for (int e = lane; e < n * n; e += 64) {
-    const int i = e / n, j = e - i * n;
-    double s = 0;
-    for (int k = 0; k < n; ++k) s = s + X[i * n + k] * Y[k * n + j];
-    Z[e] = s;
-  }
-}
+// Source of record element e of sub-controller s (same for every scenario):
+// >= 0: offset in the scenario's LDS region (Ad, Bd, Cc, fd); kZero, kOne;
+// kDx + i: observer tail element i; kY + o: plant output o.
+constexpr int kZero = -1, kOne = -2, kDx = -1000, kY = -100;
 
 template <int PLANT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams P) {
-  __shared__ double lds[kWaves * kWaveLds];
+  __shared__ double lds[kWaves * kSpw * kScnLds];
+  __shared__ int src[CMPC_MAX_S_PRODUCE * 2 * 64 * CMPC_REC_CHUNKS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x * kWaves + wave;
-  if (b >= P.B) return;  // whole wave exits together
+  const int g = lane / kLanes, l = lane - g * kLanes;  // scenario row, lane in row
+  const int b = (blockIdx.x * kWaves + wave) * kSpw + g;
+  const bool valid = b < P.B;  // (rows past the batch idle but keep the wave's syncs)
   constexpr int ns = PLANT == CMPC_PLANT_PARALLEL ? 11 : 10;
   constexpr int ni = PLANT == CMPC_PLANT_PARALLEL ? 9 : 8;
-  double* w = lds + wave * kWaveLds;
-  double *A = w, *A2 = A + kMat, *A3 = A2 + kMat, *Ac = A3 + kMat, *Ad = Ac + kMat;
+  double* w = lds + (wave * kSpw + g) * kScnLds;
+  double *A = w, *Ad = A + kMat;
   double *Bc = Ad + kMat, *Bd = Bc + 44, *Cc = Bd + 44, *fc = Cc + 44, *fd = fc + 11;
   double *xs = fd + 11, *us = xs + 11;
 
-  if (lane < ns) xs[lane] = P.x[(size_t)b * ns + lane];
-  if (lane < ni) us[lane] = P.u_full[(size_t)b * ni + lane];
+  // element -> source table (built once per workgroup)
+  for (int t = threadIdx.x; t < P.S * P.rec_len; t += 64 * kWaves) {
+    const int s = t / P.rec_len, e = t - s * P.rec_len;
+    int v = kZero;
+    const int oAd = (int)(Ad - w), oBd = (int)(Bd - w), oCc = (int)(Cc - w), ofd = (int)(fd - w);
+    if (e >= P.off_A && e < P.off_A + ns * ns) {
+      v = oAd + (e - P.off_A);
+    } else if (e >= P.off_B && e < P.off_B + ns * P.nu_tot) {
+      const int r = (e - P.off_B) / P.nu_tot, c = e - P.off_B - r * P.nu_tot;
+      v = oBd + r * 4 + P.input_order[s][c];
+    } else if (e >= P.off_C && e < P.off_C + P.ny * P.nobs) {
+      const int o = (e - P.off_C) / P.nobs, k = e - P.off_C - o * P.nobs;
+      const int oi = P.out_idx[s][o];
+      v = (k < ns) ? oCc + oi * ns + k : ((oi == k - ns) ? kOne : kZero);
+    } else if (e >= P.off_f && e < P.off_f + ns) {
+      v = ofd + (e - P.off_f);
+    } else if (e >= P.off_x && e < P.off_x + P.naug) {
+      v = kDx - (e - P.off_x);
+    } else if (e >= P.off_y && e < P.off_y + P.ny) {
+      v = kY - P.out_idx[s][e - P.off_y];
+    }
+    src[t] = v;
+  }
+  __syncthreads();
+
+  if (valid && l < ns) xs[l] = P.x[(size_t)b * ns + l];
+  if (valid && l < ni) us[l] = P.u_full[(size_t)b * ni + l];
+  for (int e = l; e < ns * ns; e += kLanes) A[e] = 0.0;  // the row clears, its lane 0
+  for (int e = l; e < ns * 4; e += kLanes) {             // writes the nonzeros
+    Bc[e] = 0.0;
+    Cc[e] = 0.0;
+  }
   WAVE_SYNC();
-  if (lane == 0) {
+#ifndef PRODUCE_EXP
+#define PRODUCE_EXP 0
+#endif
+  if (PRODUCE_EXP != 1 && valid && l == 0) {  // the scalar plant model, four scenarios side by side
     if (PLANT == CMPC_PLANT_PARALLEL)
-      cmpc_plant::parallel_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc);
+      cmpc_plant::parallel_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc, false);
     else
-      cmpc_plant::serial_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc);
+      cmpc_plant::serial_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc, false);
   }
   WAVE_SYNC();
 
   // DiscretizeRK4: Ac = Ts I + Ts^2/2 A + Ts^3/6 A^2 + Ts^4/24 A^3,
-  // Ad = I + Ac A, Bd = Ac B, fd = Ac f
+  // Ad = I + Ac A, Bd = Ac B, fd = Ac f.  Lane j of a row holds column j of
+  // [A | B | f] (j < ns: A, then the 4 B columns, then f) and, for every
+  // product row i, lane k holds X[i][k]: one row of X Y is one chain of ns
+  // DPP broadcast FMAs (k ascending, fused multiply-add like the host).
   const double Ts = P.Ts;
-  mm_wave(ns, lane, A, A, A2);
-  WAVE_SYNC();
-  mm_wave(ns, lane, A2, A, A3);
-  WAVE_SYNC();
-  for (int e = lane; e < ns * ns; e += 64) {
-    const int r = e / ns, c = e - r * ns;
-    Ac[e] = Ts * (r == c) + Ts * Ts / 2.0 * A[e] + Ts * Ts * Ts / 6.0 * A2[e] +
-            Ts * Ts * Ts * Ts / 24.0 * A3[e];
-  }
-  WAVE_SYNC();
-  mm_wave(ns, lane, Ac, A, Ad);
-  for (int e = lane; e < ns * 4 + ns; e += 64) {
-    if (e < ns * 4) {
-      const int i = e / 4, j = e - i * 4;
-      double s = 0;
-      for (int k = 0; k < ns; ++k) s = s + Ac[i * ns + k] * Bc[k * 4 + j];
-      Bd[e] = s;
-    } else {
-      const int i = e - ns * 4;
-      double s = 0;
-      for (int k = 0; k < ns; ++k) s = s + Ac[i * ns + k] * fc[k];
-      fd[i] = s;
+  if (PRODUCE_EXP != 2) {
+    double ycol[ns], a2[ns], a3[ns];
+#pragma unroll
+    for (int k = 0; k < ns; ++k)
+      ycol[k] = (l < ns) ? A[k * ns + l] : (l < ns + 4) ? Bc[k * 4 + (l - ns)]
+              : (l == ns + 4) ? fc[k] : 0.0;
+    // A^2 and A^3 (row i of X is column i of A held as ycol[i] in lane k)
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      double z = 0.0;
+      prop1_dpp<ns>(ycol[i], ycol, z);
+      a2[i] = z;
     }
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      double z = 0.0;
+      prop1_dpp<ns>(a2[i], ycol, z);
+      a3[i] = z;
+    }
+    // Ac (element-wise, lane j holds column j) and Ac [A | B | f]
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      const double ac = Ts * (i == l) + Ts * Ts / 2.0 * ycol[i] + Ts * Ts * Ts / 6.0 * a2[i] +
+                        Ts * Ts * Ts * Ts / 24.0 * a3[i];
+      double z = 0.0;
+      prop1_dpp<ns>(ac, ycol, z);
+      if (l < ns) Ad[i * ns + l] = z + (i == l ? 1.0 : 0.0);
+      else if (l < ns + 4) Bd[i * 4 + (l - ns)] = z;
+      else if (l == ns + 4) fd[i] = z;
+    }
+    WAVE_SYNC();
   }
-  WAVE_SYNC();
-  if (lane < ns) Ad[lane * ns + lane] += 1.0;
-  WAVE_SYNC();
+  if (!valid || PRODUCE_EXP == 3) return;
 
   // records of the S sub-controllers of scenario b
   for (int s = 0; s < P.S; ++s) {
     const size_t q = (size_t)b * P.S + s;
     double* rec = P.lin + q * P.rec_len;
-    for (int e = lane; e < P.rec_len; e += 64) {
-      double v = 0.0;
-      if (e >= P.off_A && e < P.off_A + ns * ns) {
-        v = Ad[e - P.off_A];
-      } else if (e >= P.off_B && e < P.off_B + ns * P.nu_tot) {
-        const int r = (e - P.off_B) / P.nu_tot, c = e - P.off_B - r * P.nu_tot;
-        v = Bd[r * 4 + P.input_order[s][c]];
-      } else if (e >= P.off_C && e < P.off_C + P.ny * P.nobs) {
-        const int o = (e - P.off_C) / P.nobs, k = e - P.off_C - o * P.nobs;
-        const int oi = P.out_idx[s][o];
-        v = (k < ns) ? Cc[oi * ns + k] : ((oi == k - ns) ? 1.0 : 0.0);
-      } else if (e >= P.off_f && e < P.off_f + ns) {
-        v = fd[e - P.off_f];
-      } else if (e >= P.off_x && e < P.off_x + P.naug) {
-        v = P.dx_aug ? P.dx_aug[q * P.naug + (e - P.off_x)] : 0.0;
-      } else if (e >= P.off_y && e < P.off_y + P.ny) {
-        v = P.y[(size_t)b * P.n_outputs + P.out_idx[s][e - P.off_y]];
-      }
+    const int* srow = src + s * P.rec_len;
+    for (int e = l; e < P.rec_len; e += kLanes) {
+      const int t = srow[e];
+      double v;
+      if (t >= 0) v = w[t];
+      else if (t == kZero) v = 0.0;
+      else if (t == kOne) v = 1.0;
+      else if (t <= kDx) v = P.dx_aug ? P.dx_aug[q * P.naug + (kDx - t)] : 0.0;
+      else v = P.y[(size_t)b * P.n_outputs + (kY - t)];
       rec[e] = v;
     }
   }
@@ -128,7 +162,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int grid = (P.B + kWaves - 1) / kWaves;
+  const int grid = (P.B + kWaves * kSpw - 1) / (kWaves * kSpw);
   if (plant == CMPC_PLANT_PARALLEL)
     hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves), 0,
                        s, P);
