@@ -28,6 +28,55 @@ from . import plant_default, plant_lin_record, plant_output, layout_of
 CONTROL_ENTRIES = (0, 3, 4, 7)   # ControlInputIndex <0,3,4,7> of both plants
 
 
+def _stable_point(cfg, dims, L, rng, x_def, u_def, out):
+    """One operating point whose discrete A has spectral radius <= 1; fills
+    out[s] with the S host-produced records and returns (x, u_full)."""
+    ns = cfg.ns
+    while True:
+        x = x_def * (1.0 + 0.01 * rng.standard_normal(x_def.shape))
+        u = u_def.copy()
+        u[list(CONTROL_ENTRIES)] += rng.uniform(-0.02, 0.02, len(CONTROL_ENTRIES))
+        for s in range(cfg.S):
+            plant_lin_record(cfg, dims, s, x, u, Ts=REF_TS, out=out[s])
+        A = out[0, L.off_A:L.off_A + ns * ns].reshape(ns, ns)
+        if np.all(np.isfinite(out)) and np.abs(np.linalg.eigvals(A)).max() <= 1.0:
+            return x, u
+
+
+def synthetic_operating_points(cfg: ControllerConfig, B: int, seed: int = 1002,
+                               n_distinct: int = None):
+    """Plant states of B scenarios (for the device producer, cmpc_produce_lin):
+    (x [B, ns], u_full [B, n_inputs], y [B, n_outputs]), drawn and filtered as
+    in synthetic_batch, n_distinct distinct points tiled over the batch."""
+    rng = np.random.default_rng(seed)
+    dims = CmpcDims.from_config(cfg, 1)
+    L = layout_of(dims)
+    nd = n_distinct or B
+    x_def, u_def = plant_default(cfg.plant)
+    xs, us, ys = [], [], []
+    scratch = np.zeros((cfg.S, L.rec_len))
+    for _ in range(nd):
+        x, u = _stable_point(cfg, dims, L, rng, x_def, u_def, scratch)
+        xs.append(x); us.append(u); ys.append(plant_output(cfg.plant, x))
+    idx = np.arange(B) % nd
+    return (np.ascontiguousarray(np.stack(xs)[idx]), np.ascontiguousarray(np.stack(us)[idx]),
+            np.ascontiguousarray(np.stack(ys)[idx]))
+
+
+def synthetic_u_old(cfg: ControllerConfig, B: int, rng) -> np.ndarray:
+    """u_old per QP slot, calibrated to the reference's closed-loop records."""
+    S = cfg.S
+    u_old = np.zeros((B, S, cfg.nu_tot))
+    for s in range(S):
+        for c, plant_c in enumerate(cfg.input_order[s]):
+            torque = plant_c in (0, 2)     # control inputs: torque1, rec1, torque2, rec2
+            if torque:
+                u_old[:, s, c] = rng.uniform(-0.098, 0.074, B)
+            else:
+                u_old[:, s, c] = np.where(rng.random(B) < 0.1, 0.0, rng.uniform(0.0, 0.066, B))
+    return np.ascontiguousarray(u_old.reshape(B * S, cfg.nu_tot))
+
+
 def synthetic_batch(cfg: ControllerConfig, B: int, seed: int = 1002, n_distinct: int = None):
     """Returns (lin [B*S, rec_len], u_old [B*S, nu_tot], du_old, ws).
 
@@ -43,17 +92,8 @@ def synthetic_batch(cfg: ControllerConfig, B: int, seed: int = 1002, n_distinct:
     x_def, u_def = plant_default(cfg.plant)
     base = np.zeros((nd, S, L.rec_len))
     ys = np.zeros((nd, 4))
-    ns = cfg.ns
     for i in range(nd):
-        while True:
-            x = x_def * (1.0 + 0.01 * rng.standard_normal(x_def.shape))
-            u = u_def.copy()
-            u[list(CONTROL_ENTRIES)] += rng.uniform(-0.02, 0.02, len(CONTROL_ENTRIES))
-            for s in range(S):
-                plant_lin_record(cfg, dims, s, x, u, Ts=REF_TS, out=base[i, s])
-            A = base[i, 0, L.off_A:L.off_A + ns * ns].reshape(ns, ns)
-            if np.all(np.isfinite(base[i])) and np.abs(np.linalg.eigvals(A)).max() <= 1.0:
-                break
+        x, _ = _stable_point(cfg, dims, L, rng, x_def, u_def, base[i])
         ys[i] = plant_output(cfg.plant, x)
     lin = np.ascontiguousarray(np.tile(base, ((B + nd - 1) // nd, 1, 1))[:B])
     idx = np.arange(B) % nd
@@ -61,15 +101,7 @@ def synthetic_batch(cfg: ControllerConfig, B: int, seed: int = 1002, n_distinct:
         lin[:, s, L.off_x:L.off_x + L.naug] = 1e-3 * rng.standard_normal((B, L.naug))
         lin[:, s, L.off_y:L.off_y + cfg.ny] = ys[idx][:, cfg.out_idx[s]]
     lin = lin.reshape(nq, L.rec_len)
-    u_old = np.zeros((B, S, cfg.nu_tot))
-    for s in range(S):
-        for c, plant_c in enumerate(cfg.input_order[s]):
-            torque = plant_c in (0, 2)     # control inputs: torque1, rec1, torque2, rec2
-            if torque:
-                u_old[:, s, c] = rng.uniform(-0.098, 0.074, B)
-            else:
-                u_old[:, s, c] = np.where(rng.random(B) < 0.1, 0.0, rng.uniform(0.0, 0.066, B))
-    u_old = np.ascontiguousarray(u_old.reshape(nq, cfg.nu_tot))
+    u_old = synthetic_u_old(cfg, B, rng)
     du_old = np.zeros((nq, cfg.nV))
     ws = np.zeros(nq, np.uint32)
     return np.ascontiguousarray(lin), u_old, du_old, ws
