@@ -81,7 +81,7 @@ EXPORTS = (
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
-    "cmpc_produce_lin", "cmpc_download_lin",
+    "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
 )
 
 _lib = None
@@ -135,6 +135,8 @@ def load_library(path: str = LIB_PATH):
                                    P(CmpcDims), P(dbl)], ctypes.c_int),
         "cmpc_produce_lin": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), c_void, c_void,
                               c_void, c_void], ctypes.c_int),
+        "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,
+                                  c_void, u32], ctypes.c_int),
         "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),
                                  P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32), ctypes.c_int,
                                  P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],

@@ -1,0 +1,123 @@
+"""Sub-controller-sharded cooperative MPC.
+
+S_total sub-controllers per scenario; each rank (one per GPU) owns S_local of
+them for all its scenarios.  The cooperative iteration's exchange
+(nerve_center.h:280-285: every sub-controller reads every other one's move
+plan) is an all-gather of the plans once per Jacobi iteration, over RCCL
+(torch.distributed "nccl") on GPUs, or gloo on CPU.
+
+The reference's plants have two compressors, so a 64-sub-controller system is
+synthetic.
+- Each sub-controller's own QP (H, f) is the coop p=50 QP of a 2-compressor
+  plant built by cmpc_build.
+- Its coupling to the other S_total - 1 sub-controllers is a dense
+  G_ext = [w_{s,1} G, ..., w_{s,S_total-1} G]. Here G is the real 4x4
+  Su'W Su_other of its own build. The weights decay with ring distance,
+  w = rho^d (1 + 0.1 * sin(1.7 b + 2.3 s + 3.1 j)), which is deterministic in
+  (scenario, s, j) and independent of the rank layout.
+"""
+import ctypes
+
+import numpy as np
+
+RHO = 0.5
+
+
+def coupling_weights(b, s, S_total: int) -> np.ndarray:
+    """w_{s,j} for the S_total - 1 other sub-controllers j (global order);
+    b, s may be arrays (broadcast over a leading axis)."""
+    b = np.asarray(b)[..., None]
+    s = np.asarray(s)[..., None]
+    j = np.arange(S_total)
+    d = np.minimum(np.abs(j - s), S_total - np.abs(j - s))
+    w = RHO ** d * (1.0 + 0.1 * np.sin(1.7 * b + 2.3 * s + 3.1 * j))
+    keep = j != s
+    return w[keep].reshape(w.shape[:-1] + (S_total - 1,))
+
+
+def synthetic_g_ext(G_local: np.ndarray, S_total: int, S_local: int, s_offset: int) -> np.ndarray:
+    """Element-major G_ext [nV*(S_total-1)*nV][nqp] for this rank's QPs
+    (q = b*S_local + local index).  G_local: (nqp, nV, nVo=nV) from the build."""
+    nqp, nV, _ = G_local.shape
+    q = np.arange(nqp)
+    b, sl = q // S_local, q % S_local
+    w = coupling_weights(b, s_offset + sl, S_total)            # (nqp, S_total-1)
+    out = np.einsum("qj,qav->ajvq", w, G_local)                # (nV, S_total-1, nV, nqp)
+    return np.ascontiguousarray(out.reshape(nV * (S_total - 1) * nV, nqp))
+
+
+def others(du_all: np.ndarray, b: int, s: int, S_total: int, S_local: int) -> np.ndarray:
+    """du_other of global sub-controller s of scenario b from rank-major
+    gathered plans du_all [world][B][S_local][nV] (as the kernel reads them)."""
+    rows = []
+    for j in range(S_total):
+        if j == s:
+            continue
+        r, sl = divmod(j, S_local)
+        rows.append(du_all[r, b, sl])
+    return np.concatenate(rows)
+
+
+def coupled_jacobi(K: int, solve_iteration, gather, du_local0):
+    """The cooperative loop of one control step: K times, gather every
+    rank's current plans (du_local: this rank's [nqp, nV]) and run one
+    Jacobi iteration on the local QPs.  solve_iteration(du_all, apply_move)
+    returns the new local plans."""
+    du_local = du_local0
+    for k in range(K):
+        du_all = gather(du_local)
+        du_local = solve_iteration(du_all, k == K - 1)
+    return du_local
+
+
+class CoupledRank:
+    """One rank of the sharded loop on its GPU: a cmpc.Context holding this
+    rank's B scenarios x S_local sub-controllers (coop dims, S = 2 setup),
+    G_ext, the local and gathered plan buffers, and the RCCL all-gather."""
+
+    def __init__(self, ctx, S_total: int, S_local: int, rank: int, world: int, G_ext, group=None):
+        import torch
+        self.torch = torch
+        self.ctx, self.S_total, self.S_local = ctx, S_total, S_local
+        self.rank, self.world, self.group = rank, world, group
+        self.s_offset = rank * S_local
+        nqp = ctx.B * ctx.cfg.S
+        if nqp % S_local:
+            raise ValueError("B*S must be a multiple of S_local")
+        self.B = nqp // S_local
+        nV = ctx.cfg.nV
+        dev = G_ext.device
+        self.G_ext = G_ext
+        self.du_local = torch.zeros(nqp, nV, dtype=torch.float64, device=dev)
+        self.du_all = torch.zeros(world, nqp, nV, dtype=torch.float64, device=dev)
+        # one stream for the library and torch's collectives
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def gather(self):
+        import torch.distributed as dist
+        if self.world == 1:
+            self.du_all[0].copy_(self.du_local)
+            return
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self.du_all, self.du_local, group=self.group)
+        else:  # gloo: CPU staging
+            parts = [self.torch.zeros_like(self.du_local, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, self.du_local.cpu(), group=self.group)
+            self.du_all.copy_(self.torch.stack(parts))
+
+    def iterate(self, apply_move: bool):
+        from . import CMPC_APPLY_MOVE
+        from ._abi import check
+        lib = self.ctx.lib
+        check(lib.cmpc_coupled_iterate(
+            self.ctx._h, self.S_total, self.S_local, self.s_offset,
+            ctypes.c_void_p(self.G_ext.data_ptr()), ctypes.c_void_p(self.du_all.data_ptr()),
+            ctypes.c_void_p(self.du_local.data_ptr()), CMPC_APPLY_MOVE if apply_move else 0),
+            "cmpc_coupled_iterate")
+
+    def step(self, K: int):
+        """build + K gathered Jacobi iterations (the first move applied)."""
+        self.ctx.build()
+        for k in range(K):
+            self.gather()
+            self.iterate(k == K - 1)

@@ -659,6 +659,47 @@ int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
   return timed_end(c, CMPC_KERNEL_ITERATE, e0);
 }
 
+int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, const double* G_ext,
+                         const double* du_all, double* du_out, uint32_t flags) {
+  if (!c) return fail("null context");
+  if (!G_ext || !du_all) return fail("cmpc_coupled_iterate: null argument");
+  if (S_local < 1 || c->nqp % S_local || S_local % c->d.S)
+    return fail("cmpc_coupled_iterate: S_local must divide B*S and be a multiple of S");
+  if (S_total < S_local || S_total % S_local || s_offset % S_local || s_offset + S_local > S_total)
+    return fail("cmpc_coupled_iterate: bad S_total / s_offset");
+  if (ensure_cfg(c)) return -1;
+  HIP_TRY(hipSetDevice(c->device));
+  CoupledParams P;
+  std::memset(&P, 0, sizeof P);
+  P.qp = c->qp;
+  P.cfg = c->cfg;
+  P.co = c->co;
+  P.u_old = c->u_old;
+  P.du_old = c->du_old;
+  P.ws = c->ws;
+  P.du = c->du;
+  P.du_out = du_out;
+  P.status = c->status;
+  P.nwsr = c->nwsr;
+  P.G_ext = G_ext;
+  P.du_all = du_all;
+  P.nqp = c->nqp;
+  P.qp_len = c->qp_len;
+  P.nu_tot = c->d.nu_tot;
+  P.S_cfg = c->d.S;
+  P.S_total = S_total;
+  P.S_local = S_local;
+  P.s_offset = s_offset;
+  P.B = c->nqp / S_local;
+  P.flags = flags;
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_ITERATE, &e0)) return -1;
+  if (cmpc_launch_coupled(P, c->L.nV, c->d.nu, c->stream))
+    return fail("coupled kernel not instantiated for these dimensions (nV = 4, nu = 2)");
+  if (check_launch("coupled kernel")) return -1;
+  return timed_end(c, CMPC_KERNEL_ITERATE, e0);
+}
+
 int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   if (cmpc_build(c)) return -1;
   return cmpc_iterate(c, K, flags);

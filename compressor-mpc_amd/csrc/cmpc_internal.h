@@ -91,10 +91,29 @@ struct ProduceParams {
   int out_idx[CMPC_MAX_S_PRODUCE][4];
 };
 
-// Kernel launchers (cmpc_kernels.hip, produce.hip).  Return 0 or -1 (unsupported dims).
+// One Jacobi iteration of the sub-controller-sharded cooperative loop
+// (coupled.hip).
+struct CoupledParams {
+  const double* qp;       // nqp * qp_len (H, f from cmpc_build)
+  const double* cfg;
+  CfgOffsets co;
+  double* u_old;          // nqp * nu_tot
+  double* du_old;         // nqp * nV
+  uint32_t* ws;
+  double* du;             // nqp * nV (context buffer)
+  double* du_out;         // nqp * nV caller buffer (the next all-gather's input) or null
+  int32_t *status, *nwsr;
+  const double* G_ext;    // [nV * (S_total-1) * nV][nqp], element-major
+  const double* du_all;   // [world][B][S_local][nV], all-gathered plans
+  int nqp, qp_len, nu_tot, S_cfg, S_total, S_local, s_offset, B;
+  uint32_t flags;
+};
+
+// Kernel launchers (cmpc_kernels.hip, produce.hip, coupled.hip).  Return 0 or -1 (unsupported dims).
 int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
                       void* stream);
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream);
+int cmpc_launch_coupled(const CoupledParams& P, int n, int nu, void* stream);

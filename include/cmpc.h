@@ -194,6 +194,24 @@ int cmpc_plant_lin_record(int plant, double p_in, double p_out, double Ts,
                           const int32_t* input_order, const int32_t* out_idx,
                           const cmpc_dims* dims, double* record);
 
+/* Sub-controller-sharded cooperative iteration.
+ * S_total sub-controllers per scenario are spread over the ranks, S_local of
+ * them on this context (QP slot q = scenario * S_local + local index; global
+ * index s_offset + local index); the context's H, f come from cmpc_build.
+ * One Jacobi iteration (nerve_center.h:146-172 with ApplyOtherInput
+ * distributed_solver.h:98-103):
+ *   f_k = f + G_ext du_other,   du = SolveQP(H, f_k) warm-started
+ * G_ext: device, [nV * (S_total-1) * nV][B*S_local] (element-major),
+ *        column block j = the j-th other sub-controller in global order.
+ * du_all: device, all-gathered plans [world][B][S_local][nV] (rank-major).
+ * du_out: device [B*S_local][nV] or NULL: this rank's new plans (the next
+ *        all-gather's input).  CMPC_APPLY_MOVE on the last iteration of a
+ *        step applies the first move (UpdateUOld) and stores du_old.
+ * The caller all-gathers between calls (RCCL; cmpc/coupled.py). */
+int cmpc_coupled_iterate(cmpc_ctx* ctx, int S_total, int S_local, int s_offset,
+                         const double* G_ext, const double* du_all, double* du_out,
+                         uint32_t flags);
+
 /* Device producer: AugmentedLinearizedSystem::Update
  * (libs/aug_lin_sys.cc:145-177, DiscretizeRK4 :232-255) for every scenario b
  * of the context's batch, on the GPU.  Linearises the plant at (x[b],

@@ -1,0 +1,219 @@
+"""Sub-controller-sharded cooperative iteration:
+S_total sub-controllers per scenario over `world` ranks, plans all-gathered
+once per Jacobi iteration (cmpc/coupled.py, coupled.hip).
+
+CPU: layout-independence of the synthetic coupling, the rank-major plan
+indexing, and the sharded loop over gloo (world size 2, the oracle's solver as
+the compute) equal to one process.  GPU: the product kernel equals the same
+loop with the oracle's solver on the product's QPs (bit-exact solver), and two
+ranks sharing the GPU equal one."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import _oracle as O
+from cmpc.coupled import coupled_jacobi, coupling_weights, others, synthetic_g_ext
+
+S_TOTAL, B, K = 8, 6, 9
+
+
+def test_coupling_weights_are_layout_independent():
+    w = coupling_weights(3, 5, S_TOTAL)
+    assert w.shape == (S_TOTAL - 1,)
+    assert np.all(w > 0) and w.max() <= 0.6
+    # the same (scenario, s, j) triple gives the same weight in any sharding
+    G = np.random.default_rng(0).normal(size=(B * S_TOTAL, 4, 4))
+    full = synthetic_g_ext(G, S_TOTAL, S_TOTAL, 0).reshape(4, (S_TOTAL - 1) * 4, B, S_TOTAL)
+    for world in (2, 4):
+        sl = S_TOTAL // world
+        for r in range(world):
+            Gr = G.reshape(B, S_TOTAL, 4, 4)[:, r * sl:(r + 1) * sl].reshape(-1, 4, 4)
+            part = synthetic_g_ext(Gr, S_TOTAL, sl, r * sl).reshape(4, (S_TOTAL - 1) * 4, B, sl)
+            assert np.array_equal(part, full[:, :, :, r * sl:(r + 1) * sl])
+
+
+def test_rank_major_plan_indexing():
+    world, sl = 4, 2
+    du_all = np.arange(world * B * sl * 4, dtype=float).reshape(world, B, sl, 4)
+    o = others(du_all, b=2, s=5, S_total=world * sl, S_local=sl)
+    expect = [du_all[j // sl, 2, j % sl] for j in range(world * sl) if j != 5]
+    assert np.array_equal(o, np.concatenate(expect))
+
+
+# ---- the loop with the oracle's solver as the compute ----------------------
+
+def problem():
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.synthetic import synthetic_batch
+    from cmpc._abi import CmpcDims
+    cfg = cmpc.reference_config("par", "coop", p=20)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    nrec = B * S_TOTAL                     # record (b, s_global) = b * S_TOTAL + s
+    lin, u_old, _, _ = synthetic_batch(cfg, nrec // cfg.S, seed=12)
+    dims = CmpcDims.from_config(cfg, 1)
+    H, f, G = [], [], []
+    for q in range(nrec):
+        h, ff, _, _, g = O.build_qp(dims, lin[q], u_old[q], arr.y_ref[q % cfg.S], arr.ywt[q % cfg.S],
+                                    arr.uwt[q % cfg.S])
+        H.append(h); f.append(ff); G.append(g)
+    return cfg, arr, np.array(H), np.array(f), np.array(G), u_old
+
+
+def oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather):
+    """This rank's QPs through coupled_jacobi with or_qp_solve (the oracle)."""
+    sl = S_TOTAL // world
+    glob = [b * S_TOTAL + rank * sl + i for b in range(B) for i in range(sl)]
+    Gx = synthetic_g_ext(G[glob], S_TOTAL, sl, rank * sl).reshape(4, -1, len(glob))
+    ws = np.zeros(len(glob), np.uint32)
+    nu = cfg.nu
+
+    def solve(du_all, apply):
+        du_all = du_all.reshape(world, B, sl, 4)
+        out = np.zeros((len(glob), 4))
+        for i, q in enumerate(glob):
+            b, li = divmod(i, sl)
+            s_cfg = q % cfg.S
+            d = others(du_all, b, rank * sl + li, S_TOTAL, sl)
+            fk = [float(v) for v in f[q]]
+            for j in range(S_TOTAL - 1):          # the kernel's order: j, then a, then v
+                for a in range(4):
+                    for v in range(4):
+                        fk[a] = fk[a] + float(Gx[a, j * 4 + v, i]) * float(d[j * 4 + v])
+            lo = np.tile(arr.lower[s_cfg] - u_old[q, :nu], 2)
+            up = np.tile(arr.upper[s_cfg] - u_old[q, :nu], 2)
+            x, info = O.qp_solve(H[q], np.array(fk), lo, up, np.tile(arr.rate_lower[s_cfg], 2),
+                                 np.tile(arr.rate_upper[s_cfg], 2), nu, int(ws[i]))
+            ws[i] = info.ws
+            out[i] = x
+        return out
+
+    return coupled_jacobi(K, solve, gather, np.zeros((len(glob), 4)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cpu_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg, arr, H, f, G, u_old = problem()
+
+        def gather(du_local):
+            parts = [torch.zeros(du_local.shape, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(du_local)))
+            return torch.stack(parts).numpy()
+
+        du = oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather)
+        allp = gather(du)
+        if rank == 0:
+            q.put(allp)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_loop_two_ranks_gloo_equals_one():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=600)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cfg, arr, H, f, G, u_old = problem()
+    ref = oracle_loop(cfg, arr, H, f, G, u_old, 0, 1, lambda d: d[None])
+    # rank-major [world][B][sl][4] -> global [B][S_TOTAL][4]
+    sl = S_TOTAL // world
+    got = got.reshape(world, B, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
+    assert np.array_equal(got, ref)
+
+
+# ---- GPU: the product kernel -----------------------------------------------
+
+def product_rank(rank, world, group_gather=None):
+    import torch
+    import cmpc
+    from cmpc.coupled import CoupledRank
+    cfg, arr, H, f, G, u_old = problem()
+    sl = S_TOTAL // world
+    glob = [b * S_TOTAL + rank * sl + i for b in range(B) for i in range(sl)]
+    from cmpc.synthetic import synthetic_batch
+    lin, _, _, _ = synthetic_batch(cfg, B * S_TOTAL // cfg.S, seed=12)
+    ctx = cmpc.Context(cfg, len(glob) // cfg.S, device=0)
+    ctx.configure(arr)
+    ctx.set_state(np.ascontiguousarray(u_old[glob]), np.zeros((len(glob), cfg.nV)),
+                  np.zeros(len(glob), np.uint32))
+    ctx.upload_lin(np.ascontiguousarray(lin[glob]))
+    ctx.build()
+    Hd, fd, Gd = ctx.download_qp()
+    Gx = torch.from_numpy(synthetic_g_ext(Gd, S_TOTAL, sl, rank * sl)).cuda()
+    cr = CoupledRank(ctx, S_TOTAL, sl, rank, world, Gx)
+    cr.step(K)
+    torch.cuda.synchronize()
+    return cfg, arr, ctx, cr, Hd, fd, Gd, u_old[glob]
+
+
+@pytest.mark.gpu
+def test_gpu_coupled_kernel_equals_oracle_loop():
+    cfg, arr, ctx, cr, Hd, fd, Gd, u_g = product_rank(0, 1)
+    du_gpu = cr.du_local.cpu().numpy()
+    # the oracle loop on the product's own QPs
+    n = len(u_g)
+    glob = list(range(n))
+    H = np.zeros((n, 4, 4)); f = np.zeros((n, 4)); G = np.zeros((n, 4, 4))
+    H[:], f[:], G[:] = Hd, fd, Gd
+    ref = oracle_loop(cfg, arr, H, f, G, np.ascontiguousarray(u_g), 0, 1, lambda d: d[None])
+    ctx.close()
+    assert np.array_equal(du_gpu, ref)
+
+
+def _gpu_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, _, ctx, cr, *_ = product_rank(rank, world)
+        parts = [torch.zeros(cr.du_local.shape, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, cr.du_local.cpu())
+        if rank == 0:
+            q.put(torch.stack(parts).numpy())
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_coupled_two_ranks_equal_one():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=600)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    *_, ctx1, cr1, _, _, _, _ = product_rank(0, 1)
+    one = cr1.du_local.cpu().numpy()
+    ctx1.close()
+    sl = S_TOTAL // world
+    got = got.reshape(world, B, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
+    assert np.array_equal(got, one)
