@@ -239,7 +239,9 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
   if (L.nd > CMPC_ND_MAX) return fail("more than 4 delayed inputs");
   if (d.ns + d.nu_tot > 15) return fail("ns + nu_tot must be <= 15 (16-lane DPP rows)");
   if (d.m * d.nu_tot + 1 > 16) return fail("m * nu_tot + 1 must be <= 16 (gather lanes of a DPP row)");
-  if (d.ny > 3) return fail("ny > 3 is not instantiated in the build kernel");
+  if (d.ny > 4) return fail("ny > 4 is not instantiated in the build kernel (one DPP row per output)");
+  if (d.ns + d.ny + L.nd > 16)
+    return fail("ns + ny + (delayed inputs) must be <= 16 (free-response DPP row)");
   const long long nqp = (long long)d.B * d.S;
   if (nqp > (1LL << 30)) return fail("batch too large");
   int ndev = 0;
@@ -539,7 +541,18 @@ static void build_lds_layout(const cmpc_dims& d, const cmpc_layout& L, BuildPara
   o += up((d.p + 3) * d.ny, 2);
   while (o % 32 != (M * nut) % 32) o += 2;               // z slots next to row 0's window
   P->zs_off = o;
-  o += d.ny * 4;
+  if (d.ny == 4) {
+    // pre-pass z lines: stride = 1 mod 32, so row o's z read sits at residue
+    // m*nu_tot + o (between the line windows of rows o and o+1 at 0 / 16 mod 32)
+    // and the four writes of a step hit distinct banks
+    int zst = d.p;
+    while (zst % 32 != 1) ++zst;
+    P->zl_stride = zst;
+    o += d.ny * zst;
+  } else {
+    P->zl_stride = 4;
+    o += d.ny * 4;
+  }
   P->lds_per_wave = up(o, 32);
   P->yl_stride = up((d.p + 1) * d.ny, 32);
   P->lds_block = up(d.S * P->yl_stride + d.S * d.ny * d.ny + d.S * d.nu * d.nu + 16, 32);

@@ -40,7 +40,9 @@ struct BuildParams {
   int line_off[CMPC_MAX_INPUTS]; // delay line of input c inside a row
   int line_rs;                   // delay-line row stride (one row per output)
   int w_off;                     // w table
-  int zs_off;                    // free-response hand-off slots (NY x 4)
+  int zs_off;                    // free-response hand-off slots (NY x 4), or the
+                                 // ny = 4 pre-pass z lines (NY x zl_stride)
+  int zl_stride;
   int nbound;                    // distinct delays 0 < D < p, ascending (loop segments)
   int bound[CMPC_MAX_INPUTS];
   int grid;                      // workgroups needed (one QP per wave); launcher caps it

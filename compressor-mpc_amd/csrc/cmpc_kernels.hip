@@ -86,6 +86,11 @@ void cmpc_build_kernel(BuildParams P) {
   constexpr int U = 4;                  // horizon-loop unroll (immediate LDS offsets)
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   static_assert(ND <= NY, "w table shares the yhat stride");
+  static_assert(NY <= 4, "one DPP row per output");
+  // ny = 4 leaves no DPP row for the free response: it then runs as a
+  // pre-pass (every row simulating, row 3 storing z_r into per-output lines)
+  // and the main pass has four P rows whose z lanes read those lines
+  constexpr bool PRE = NY == 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int row = lane >> 4, col = lane & 15;
@@ -151,7 +156,7 @@ void cmpc_build_kernel(BuildParams P) {
 
   // ---- static lane roles and LDS gather descriptors (same for every QP) ----
   const bool prow = row < NY;
-  const bool srow = row == 3;
+  const bool srow = !PRE && row == 3;
   const int c_in = col - NS;
   const bool mlane = prow && col >= NS && col < NS + NUT;       // raw Markov writer
   const bool slane = srow && col >= NS && col < NS + NY;        // free-response writer
@@ -197,6 +202,9 @@ void cmpc_build_kernel(BuildParams P) {
       gdel = P.delay[c];
       smask = (k == M - 1) ? 1.0 : 0.0;
       if (gdel == 0) { rp = rline; rinc = 1; }
+    } else if (PRE) {
+      rp = zl + row * P.zl_stride;  // z line of output row, one entry per step
+      rinc = 1;
     } else {
       rp = zl + row * U;
     }
@@ -283,6 +291,53 @@ void cmpc_build_kernel(BuildParams P) {
         if (o2 >= row) t += lwt[row * NY + o2] * yp[o2];
       kap[row] = t;
     }
+    if constexpr (PRE) {
+      // free-response pre-pass: the row-3 lane roles of the ny <= 3 layout in
+      // every row (states j < ns, outputs ns + o, delayed-input carriers in
+      // the top ND lanes); row 3's output lanes store z_r at zl[o][r]
+      const bool s_st = col < NS, s_out = col >= NS && col < NS + NY, s_w = col >= 16 - ND;
+      const int soz = s_out ? col - NS : 0, skw = s_w ? col - (16 - ND) : 0;
+      const double sym = s_out ? 1.0 : s_w ? -1.0 : 0.0;
+      const double* smb = s_st ? recl + P.off_A + col * NS : s_out ? chat + soz * nobs : zero_p;
+      const int sms = (s_st || s_out) ? 1 : 0;
+      const double* sad = s_st ? recl + P.off_B + col * NUT : zero_p;
+      double sm[NS + NDW];
+#pragma unroll
+      for (int l = 0; l < NS; ++l) sm[l] = smb[l * sms];
+#pragma unroll
+      for (int k = 0; k < NDW; ++k) sm[NS + k] = (ND > 0) ? sad[s_st ? wdi[k] : 0] : 0.0;
+      const double sbase = *(s_st ? recl + P.off_f + col : s_out ? kap + soz : zero_p);
+      double spv = *(s_st ? recl + P.off_f + col : s_w ? wl + NY + skw : zero_p);
+#pragma unroll
+      for (int k = 0; k < ND; ++k) spv += sm[NS + k] * wl[k];  // x_1 = f + Adelay w_0
+      double syh = s_w ? wl[2 * NY + skw] : yl[soz];
+      const double* sylp = s_w ? wl + 3 * NY + skw : yl + NY + soz;
+      const bool zlane = row == 3 && s_out;
+      double* zq = zl + soz * P.zl_stride;
+#define CMPC_PRE_STEP(u)                          \
+  {                                               \
+    double a = __builtin_fma(-sym, syh, sbase);   \
+    prop1w_dpp<NS, ND>(spv, sm, a);               \
+    syh = sylp[(u) * NY];                         \
+    spv = a;                                      \
+    if (zlane) zq[u] = a;                         \
+  }
+      int r = 0;
+      for (; r + U <= pp; r += U) {
+        CMPC_PRE_STEP(0)
+        CMPC_PRE_STEP(1)
+        CMPC_PRE_STEP(2)
+        CMPC_PRE_STEP(3)
+        zq += U;
+        sylp += U * NY;
+      }
+      for (; r < pp; ++r) {
+        CMPC_PRE_STEP(0)
+        zq += 1;
+        sylp += NY;
+      }
+#undef CMPC_PRE_STEP
+    }
     // per-lane operands (branch-free gathers through the descriptors)
     // m[NS + k] = Adelay[j][k]: the sim row's state lanes pick up w_{r+1}
     // from the carrier lanes 16 - ND + k inside the DPP chain
@@ -319,7 +374,7 @@ void cmpc_build_kernel(BuildParams P) {
     /* accumulate row r-1: acc[a] += column_a * own column (gather lanes) */          \
     va = __builtin_fma(smask, va, rd);                                                 \
     CMPC_EXP_STEP(pv, m, a, va, acc);                                                  \
-    CMPC_EXP_YH(yh = ylp[(u) * NY]);                                                   \
+    CMPC_EXP_YH(if constexpr (!PRE) yh = ylp[(u) * NY]);                               \
     /* a: P rows -> P_{r+1} / raw Markov of step r; sim lanes -> x_{r+2} / z_r */      \
     pv = a;                                                                            \
     CMPC_EXP_HAND(if (mlane || slane) wq[u] = a; rd = rq[u];)                          \
@@ -584,6 +639,8 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m, void*
   BUILD_CASE(11, 2, 2, 2)  // parallel ncoop       (NCControlledOutputIndices)
   BUILD_CASE(11, 3, 4, 2)  // parallel centralized
   BUILD_CASE(10, 2, 2, 2)  // serial ncoop
+  BUILD_CASE(10, 4, 2, 2)  // serial coop          (NullIndexArray<4>: all four outputs)
+  BUILD_CASE(10, 4, 4, 2)  // serial centralized
   BUILD_CASE(11, 3, 2, 1)
   BUILD_CASE(11, 3, 2, 3)
   return -1;

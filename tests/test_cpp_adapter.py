@@ -77,7 +77,7 @@ def test_setup_writer_roundtrip(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "ncoop-ser"])
+@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser"])
 def test_gpu_cpp_adapter_step0_matches_reference(name, tmp_path):
     _build()
     cfg, _, _, g = GC.case(name)

@@ -33,7 +33,7 @@ def make_ctx(cfg, arr, B, lin, u_old, du_old, ws):
     return ctx
 
 
-GPU_GOLDEN = ("cent-par", "coop-par", "ncoop-par", "ncoop-ser")
+GPU_GOLDEN = ("cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser")
 
 
 @pytest.mark.parametrize("name", GPU_GOLDEN)
@@ -66,7 +66,8 @@ def oracle_qps(cfg, arr, lin, u_old):
 
 
 BUILD_CASES = [("par", "coop", 20), ("par", "coop", 50), ("par", "ncoop", 50),
-               ("par", "cent", 50), ("par", "coop", 100), ("ser", "ncoop", 50)]
+               ("par", "cent", 50), ("par", "coop", 100), ("ser", "ncoop", 50),
+               ("ser", "coop", 50), ("ser", "cent", 50), ("ser", "coop", 100)]
 
 
 def setup_for(plant, ctype):
@@ -163,7 +164,8 @@ def test_gpu_solver_status_paths():
 
 
 STEP_CASES = [("par", "coop", 20, 9), ("par", "coop", 50, 9), ("par", "ncoop", 50, 9),
-              ("par", "cent", 50, 1), ("ser", "ncoop", 50, 9)]
+              ("par", "cent", 50, 1), ("ser", "ncoop", 50, 9),
+              ("ser", "coop", 50, 9), ("ser", "cent", 50, 1)]
 
 
 @pytest.mark.parametrize("plant,ctype,p,K", STEP_CASES)
@@ -253,10 +255,11 @@ def test_gpu_large_batch_properties():
 
 
 # SURVEY.md §8(d) configs restated as parity cases (the bench line is config
-# "coop p=50"; these run at their own sizes): (2) coop-par p=20 B=4096 K=9,
-# (3) ncoop-par p=50 B=65536 K=1, (5) cent-par p=200 B=1024 K=1.
-SURVEY_CONFIGS = [("par", "coop", 20, 4096, 9), ("par", "ncoop", 50, 65536, 1),
-                  ("par", "cent", 200, 1024, 1)]
+# "coop p=50"; these run at their own sizes): (1) cent-ser at the reference's
+# p=100 (its CPU timing case, here batched B=4096), (2) coop-par p=20 B=4096
+# K=9, (3) ncoop-par p=50 B=65536 K=1, (5) cent-par p=200 B=1024 K=1.
+SURVEY_CONFIGS = [("ser", "cent", 100, 4096, 1), ("par", "coop", 20, 4096, 9),
+                  ("par", "ncoop", 50, 65536, 1), ("par", "cent", 200, 1024, 1)]
 
 
 @pytest.mark.parametrize("plant,ctype,p,B,K", SURVEY_CONFIGS)

@@ -14,7 +14,8 @@ import cmpc
 from cmpc._abi import CmpcDims
 from cmpc.configs import reference_setup
 
-CASES = [("par", "coop"), ("par", "ncoop"), ("par", "cent"), ("ser", "ncoop")]
+CASES = [("par", "coop"), ("par", "ncoop"), ("par", "cent"), ("ser", "ncoop"), ("ser", "coop"),
+         ("ser", "cent")]
 CTRL = [0, 3, 4, 7]  # ControlInputIndex of both plants
 
 
