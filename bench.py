@@ -213,6 +213,49 @@ def main():
                   "note": "device producer (plant linearisation + discretisation + records) + build "
                           "+ K iterations with the move applied; synthetic plant states held fixed "
                           "(no plant simulation), so applied moves accumulate step to step"}
+        # the full receding-horizon step with the per-sub-controller observer
+        # (SURVEY §8(f) row 2): a posteriori update + linearisation at each
+        # slot's x_hat, build, K iterations, a priori update + u_old += du
+        try:
+            L0 = ctx.layout
+            rng_o = np.random.default_rng(79 + rank)
+            for s_ in range(S):
+                ctx.set_observer(s_, 0.01 * rng_o.standard_normal((L0.nobs, ys.shape[1])))
+            ctx.set_state(synthetic_u_old(cfg, B, np.random.default_rng(78 + rank)),
+                          np.zeros((B * S, cfg.nV)), np.zeros(B * S, np.uint32))
+            ctx.observer_init(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+            ctx.build()
+            ctx.init_warmstart()
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+            ctx.synchronize()
+            t_os = (time.perf_counter() - t0) / reps
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.observe_apply()
+            ctx.synchronize()
+            t_oa = (time.perf_counter() - t0) / reps
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+                ctx.build()
+                ctx.iterate(K)
+                ctx.observe_apply()
+            ctx.synchronize()
+            t_full = (time.perf_counter() - t0) / reps
+            _, st_o, _ = ctx.download()
+            closed["with_observer"] = {
+                "ms_per_step": t_full * 1e3, "observe_step_ms": t_os * 1e3,
+                "observe_apply_ms": t_oa * 1e3,
+                "qp_status_ok_fraction": float((st_o == 0).mean()),
+                "qp_solves_per_s": B * S * K / t_full,
+                "note": "observe a posteriori + per-QP linearisation at x_hat (records), build, "
+                        "K iterations, observe a priori + u_old update; measured y held fixed, "
+                        f"random observer gain (0.01 scale), {reps} consecutive steps"}
+        except Exception as e:
+            log(f"observer closed-loop variant failed: {e}")
     except Exception as e:  # reported, never required
         log(f"closed-loop variant failed: {e}")
     ok_frac = float((st == 0).mean())

@@ -85,6 +85,21 @@ def qp_solve_batch(H, g, lb, ub, lbA, ubA, nu, ws_in=None, max_chg=10, device=0)
     return x, status, nchg, ws_out, trace, ntrace
 
 
+def _torch_runtime_first():
+    """torch bundles its own HIP runtime; when the library's runtime opens the
+    device first, torch's later initialisation reports no GPUs.  If the
+    caller uses torch for device buffers (it is imported), bring its runtime
+    up before the library's."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+
+
 class Context:
     """One batched NerveCenter over B scenarios of cfg.S sub-controllers."""
 
@@ -96,6 +111,7 @@ class Context:
         self.layout = layout_of(self.dims)
         self.nqp = B * cfg.S
         self._h = ctypes.c_void_p()
+        _torch_runtime_first()
         check(self.lib.cmpc_create(ctypes.byref(self._h), ctypes.byref(self.dims), device),
               "cmpc_create")
 
@@ -169,6 +185,47 @@ class Context:
             self._h, self.cfg.plant, p_in, p_out, Ts, iptr(io), iptr(oi), ctypes.c_void_p(x_ptr),
             ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(dx_aug_ptr or None), ctypes.c_void_p(y_ptr)),
             "cmpc_produce_lin")
+
+    # -- observer + receding-horizon update --------
+    def set_observer(self, s: int, M: np.ndarray):
+        """ObserverMatrix of sub-controller s, (ns + ndist) x n_outputs."""
+        M = np.ascontiguousarray(M, dtype=np.float64)
+        check(self.lib.cmpc_set_observer(self._h, s, M.shape[1], dptr(M)), "cmpc_set_observer")
+
+    @property
+    def observer_len(self) -> int:
+        return self.lib.cmpc_observer_len(self._h)
+
+    def observer_init(self, x_ptr: int, u_full_ptr: int, y_ptr: int, dx_init_ptr: int = 0,
+                      Ts: float = 0.05, p_in: float = 1.0, p_out: float = 1.0):
+        """DistributedController::Initialize for every slot: observer state at
+        (x_init[b], y_init[b], dx_init) and the records at x_init (device ptrs)."""
+        io = np.ascontiguousarray(self.cfg.input_order, dtype=np.int32)
+        oi = np.ascontiguousarray(self.cfg.out_idx, dtype=np.int32)
+        check(self.lib.cmpc_observer_init(
+            self._h, self.cfg.plant, p_in, p_out, Ts, iptr(io), iptr(oi), ctypes.c_void_p(x_ptr),
+            ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(y_ptr), ctypes.c_void_p(dx_init_ptr or None)),
+            "cmpc_observer_init")
+
+    def observe_step(self, u_full_ptr: int, y_ptr: int):
+        """ObserveAPosteriori + x_hat update, then the records at x_hat."""
+        check(self.lib.cmpc_observe_step(self._h, ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(y_ptr)),
+              "cmpc_observe_step")
+
+    def observe_apply(self):
+        """UpdateU: ObserveAPriori with the own first move, then u_old += du."""
+        check(self.lib.cmpc_observe_apply(self._h), "cmpc_observe_apply")
+
+    def observer_state(self) -> np.ndarray:
+        """(B*S, observer_len): [x_hat ns][dx_aug ntot][y_old n_out][C n_out x ns]."""
+        out = np.zeros((self.B * self.cfg.S, self.observer_len))
+        check(self.lib.cmpc_get_observer_state(self._h, dptr(out)), "cmpc_get_observer_state")
+        return out
+
+    def set_observer_state(self, st: np.ndarray):
+        st = np.ascontiguousarray(st, dtype=np.float64)
+        assert st.shape == (self.B * self.cfg.S, self.observer_len)
+        check(self.lib.cmpc_set_observer_state(self._h, dptr(st)), "cmpc_set_observer_state")
 
     def download_lin(self) -> np.ndarray:
         """The context's own record buffer (B*S, rec_len), e.g. after produce_lin."""

@@ -82,6 +82,8 @@ EXPORTS = (
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
+    "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
+    "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
 )
 
 _lib = None
@@ -135,6 +137,14 @@ def load_library(path: str = LIB_PATH):
                                    P(CmpcDims), P(dbl)], ctypes.c_int),
         "cmpc_produce_lin": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), c_void, c_void,
                               c_void, c_void], ctypes.c_int),
+        "cmpc_set_observer": ([c_void, ctypes.c_int, ctypes.c_int, P(dbl)], ctypes.c_int),
+        "cmpc_observer_len": ([c_void], ctypes.c_int),
+        "cmpc_observer_init": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), c_void, c_void,
+                                c_void, c_void], ctypes.c_int),
+        "cmpc_observe_step": ([c_void, c_void, c_void], ctypes.c_int),
+        "cmpc_observe_apply": ([c_void], ctypes.c_int),
+        "cmpc_get_observer_state": ([c_void, P(dbl)], ctypes.c_int),
+        "cmpc_set_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,
                                   c_void, u32], ctypes.c_int),
         "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),

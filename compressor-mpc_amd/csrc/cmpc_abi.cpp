@@ -86,6 +86,15 @@ struct cmpc_ctx {
   uint8_t* trace = nullptr;
   size_t trace_cap = 0;
   int trace_K = 0;
+  // observer (cmpc_set_observer / cmpc_observer_init)
+  int obs_nout = 0, obs_len = 0, obs_plant = -1;
+  double obs_pin = 0, obs_pout = 0, obs_Ts = 0;
+  std::vector<double> obsM;  // S x nobs x n_out
+  std::vector<int> have_M;
+  bool obsM_dirty = true;
+  double *d_obsM = nullptr, *obs = nullptr;
+  int obs_io[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS] = {};
+  int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
@@ -317,7 +326,7 @@ int cmpc_destroy(cmpc_ctx* c) {
     }
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
-                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace};
+                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace, c->obs, c->d_obsM};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -441,54 +450,242 @@ int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
   return 0;
 }
 
+static int fill_produce(cmpc_ctx* c, const char* who, int plant, double p_in, double p_out,
+                        double Ts, const int32_t* input_order, const int32_t* out_idx,
+                        ProduceParams* P, int* n_outputs) {
+  const cmpc_dims& d = c->d;
+  const cmpc_layout& L = c->L;
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(plant, &ns, &ni, &no, &nci)) return fail(std::string(who) + ": unknown plant");
+  if (d.ns != ns || d.nu_tot != nci || d.ndist > no || d.ny > 4)
+    return fail(std::string(who) + ": context dimensions do not match the plant");
+  if (d.S > CMPC_MAX_S_PRODUCE) return fail(std::string(who) + ": too many sub-controllers");
+  std::memset(P, 0, sizeof *P);
+  P->lin = c->lin;
+  P->B = d.B;
+  P->S = d.S;
+  P->rec_len = L.rec_len;
+  P->nu_tot = d.nu_tot;
+  P->ny = d.ny;
+  P->nobs = L.nobs;
+  P->naug = L.naug;
+  P->n_outputs = no;
+  P->off_A = L.off_A; P->off_B = L.off_B; P->off_C = L.off_C;
+  P->off_f = L.off_f; P->off_x = L.off_x; P->off_y = L.off_y;
+  P->p_in = p_in;
+  P->p_out = p_out;
+  P->Ts = Ts;
+  for (int s = 0; s < d.S; ++s) {
+    for (int k = 0; k < d.nu_tot; ++k) {
+      const int v = input_order[s * d.nu_tot + k];
+      if (v < 0 || v >= nci) return fail(std::string(who) + ": bad input_order");
+      P->input_order[s][k] = v;
+    }
+    for (int o = 0; o < d.ny; ++o) {
+      const int v = out_idx[s * d.ny + o];
+      if (v < 0 || v >= no) return fail(std::string(who) + ": bad out_idx");
+      P->out_idx[s][o] = v;
+    }
+  }
+  if (n_outputs) *n_outputs = no;
+  return 0;
+}
+
 int cmpc_produce_lin(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
                      const int32_t* input_order, const int32_t* out_idx, const double* x,
                      const double* u_full, const double* dx_aug, const double* y) {
   if (!c) return fail("null context");
   if (!input_order || !out_idx || !x || !u_full || !y) return fail("cmpc_produce_lin: null argument");
-  const cmpc_dims& d = c->d;
-  const cmpc_layout& L = c->L;
-  int ns = 0, ni = 0, no = 0, nci = 0;
-  if (cmpc_plant_dims(plant, &ns, &ni, &no, &nci)) return fail("cmpc_produce_lin: unknown plant");
-  if (d.ns != ns || d.nu_tot != nci || d.ndist > no || d.ny > 4)
-    return fail("cmpc_produce_lin: context dimensions do not match the plant");
-  if (d.S > CMPC_MAX_S_PRODUCE) return fail("cmpc_produce_lin: too many sub-controllers");
   ProduceParams P;
-  std::memset(&P, 0, sizeof P);
-  P.lin = c->lin;
+  if (fill_produce(c, "cmpc_produce_lin", plant, p_in, p_out, Ts, input_order, out_idx, &P, nullptr))
+    return -1;
   P.x = x;
   P.u_full = u_full;
   P.dx_aug = dx_aug;
   P.y = y;
-  P.B = d.B;
-  P.S = d.S;
-  P.rec_len = L.rec_len;
-  P.nu_tot = d.nu_tot;
-  P.ny = d.ny;
-  P.nobs = L.nobs;
-  P.naug = L.naug;
-  P.n_outputs = no;
-  P.off_A = L.off_A; P.off_B = L.off_B; P.off_C = L.off_C;
-  P.off_f = L.off_f; P.off_x = L.off_x; P.off_y = L.off_y;
-  P.p_in = p_in;
-  P.p_out = p_out;
-  P.Ts = Ts;
-  for (int s = 0; s < d.S; ++s) {
-    for (int k = 0; k < d.nu_tot; ++k) {
-      const int v = input_order[s * d.nu_tot + k];
-      if (v < 0 || v >= nci) return fail("cmpc_produce_lin: bad input_order");
-      P.input_order[s][k] = v;
-    }
-    for (int o = 0; o < d.ny; ++o) {
-      const int v = out_idx[s * d.ny + o];
-      if (v < 0 || v >= no) return fail("cmpc_produce_lin: bad out_idx");
-      P.out_idx[s][o] = v;
-    }
-  }
   HIP_TRY(hipSetDevice(c->device));
   c->lin_bound = nullptr;  // the build reads the produced records
   if (cmpc_launch_produce(P, plant, c->stream)) return fail("cmpc_produce_lin: launch failed");
   return check_launch("produce kernel");
+}
+
+// ---- observer ----
+static void observer_params(cmpc_ctx* c, ObserverParams* P) {
+  const cmpc_dims& d = c->d;
+  const cmpc_layout& L = c->L;
+  std::memset(P, 0, sizeof *P);
+  P->obs = c->obs;
+  P->M = c->d_obsM;
+  P->lin = c->lin;
+  P->du_old = c->du_old;
+  P->u_old = c->u_old;
+  P->nqp = c->nqp;
+  P->S = d.S;
+  P->ns = d.ns;
+  P->ndist = d.ndist;
+  P->nobs = L.nobs;
+  P->ntot = L.ntot;
+  P->n_out = c->obs_nout;
+  P->obs_len = c->obs_len;
+  P->nu = d.nu;
+  P->nu_tot = d.nu_tot;
+  P->nV = L.nV;
+  P->rec_len = L.rec_len;
+  P->off_B = L.off_B;
+  P->off_f = L.off_f;
+  int blk = L.nobs + L.nd;
+  for (int i = 0; i < d.nu_tot; ++i) {
+    P->delay[i] = d.delay[i];
+    if (d.delay[i]) {
+      P->dinput[P->nd] = i;
+      P->blk[P->nd] = blk;
+      blk += d.delay[i] - 1;
+      P->nd++;
+    }
+  }
+}
+
+static int observer_upload_M(cmpc_ctx* c) {
+  for (int s = 0; s < c->d.S; ++s)
+    if (!c->have_M[s]) return fail("observer gain of sub-controller " + std::to_string(s) + " not set");
+  if (c->obsM_dirty) {
+    HIP_TRY(hipMemcpyAsync(c->d_obsM, c->obsM.data(), sizeof(double) * c->obsM.size(),
+                           hipMemcpyHostToDevice, c->stream));
+    c->obsM_dirty = false;
+  }
+  return 0;
+}
+
+int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
+  if (!c || !M) return fail("null argument");
+  const cmpc_dims& d = c->d;
+  if (s < 0 || s >= d.S) return fail("cmpc_set_observer: bad sub-controller index");
+  if (n_outputs < 1 || n_outputs > 8 || n_outputs < d.ndist)
+    return fail("cmpc_set_observer: n_outputs must be in [ndist, 8]");
+  if (c->obs_nout && c->obs_nout != n_outputs)
+    return fail("cmpc_set_observer: n_outputs differs between sub-controllers");
+  if (c->L.nobs > 32) return fail("cmpc_set_observer: ns + ndist > 32");
+  for (int i = 0; i < d.nu_tot; ++i)
+    if (d.delay[i] == 1) return fail("cmpc_set_observer: a one-step input delay has no delay block");
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->obs) {
+    c->obs_nout = n_outputs;
+    c->obs_len = (d.ns + c->L.ntot + n_outputs + n_outputs * d.ns + 1) / 2 * 2;
+    c->obsM.assign((size_t)d.S * c->L.nobs * n_outputs, 0.0);
+    c->have_M.assign(d.S, 0);
+    HIP_TRY(hipMalloc(&c->d_obsM, sizeof(double) * c->obsM.size()));
+    HIP_TRY(hipMalloc(&c->obs, sizeof(double) * (size_t)c->nqp * c->obs_len));
+    HIP_TRY(hipMemsetAsync(c->obs, 0, sizeof(double) * (size_t)c->nqp * c->obs_len, c->stream));
+  }
+  std::memcpy(c->obsM.data() + (size_t)s * c->L.nobs * n_outputs, M,
+              sizeof(double) * c->L.nobs * n_outputs);
+  c->have_M[s] = 1;
+  c->obsM_dirty = true;
+  return 0;
+}
+
+int cmpc_observer_len(const cmpc_ctx* c) { return c ? c->obs_len : 0; }
+
+// linearise every QP slot at its own x_hat (observer state) and store C
+static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) {
+  ProduceParams P;
+  int no = 0;
+  int io[CMPC_MAX_S_PRODUCE * CMPC_MAX_INPUTS], oi[CMPC_MAX_S_PRODUCE * 4];
+  for (int s = 0; s < c->d.S; ++s) {
+    for (int k = 0; k < c->d.nu_tot; ++k) io[s * c->d.nu_tot + k] = c->obs_io[s][k];
+    for (int o = 0; o < c->d.ny; ++o) oi[s * c->d.ny + o] = c->obs_oi[s][o];
+  }
+  if (fill_produce(c, "observer", c->obs_plant, c->obs_pin, c->obs_pout, c->obs_Ts, io, oi, &P, &no))
+    return -1;
+  P.per_qp = 1;
+  P.x = c->obs;
+  P.x_stride = c->obs_len;
+  P.dx_aug = c->obs + c->d.ns + c->d.ns;  // dx_aug tail (aug states) of slot 0
+  P.dx_stride = c->obs_len;
+  P.c_out = c->obs + c->d.ns + c->L.ntot + c->obs_nout;
+  P.c_stride = c->obs_len;
+  P.u_full = u_full;
+  P.y = y;
+  c->lin_bound = nullptr;
+  if (cmpc_launch_produce(P, c->obs_plant, c->stream)) return fail("observer: produce launch failed");
+  return check_launch("produce kernel (per QP)");
+}
+
+int cmpc_observer_init(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
+                       const int32_t* input_order, const int32_t* out_idx, const double* x_init,
+                       const double* u_full, const double* y_init, const double* dx_init) {
+  if (!c) return fail("null context");
+  if (!input_order || !out_idx || !x_init || !u_full || !y_init)
+    return fail("cmpc_observer_init: null argument");
+  if (!c->obs) return fail("cmpc_observer_init: set the observer gains first (cmpc_set_observer)");
+  ProduceParams chk;
+  int no = 0;
+  if (fill_produce(c, "cmpc_observer_init", plant, p_in, p_out, Ts, input_order, out_idx, &chk, &no))
+    return -1;
+  if (no != c->obs_nout) return fail("cmpc_observer_init: plant outputs differ from the observer gains' n_outputs");
+  c->obs_plant = plant;
+  c->obs_pin = p_in;
+  c->obs_pout = p_out;
+  c->obs_Ts = Ts;
+  for (int s = 0; s < c->d.S; ++s) {
+    for (int k = 0; k < c->d.nu_tot; ++k) c->obs_io[s][k] = chk.input_order[s][k];
+    for (int o = 0; o < c->d.ny; ++o) c->obs_oi[s][o] = chk.out_idx[s][o];
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if (observer_upload_M(c)) return -1;
+  ObserverParams P;
+  observer_params(c, &P);
+  P.x_init = x_init;
+  P.dx_init = dx_init;
+  P.y = y_init;
+  if (cmpc_launch_observer(P, CMPC_OBS_INIT, c->stream)) return fail("observer init launch failed");
+  if (check_launch("observer init kernel")) return -1;
+  return observer_produce(c, u_full, y_init);  // Initialize: Update(x_init, full_u_old)
+}
+
+int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
+  if (!c) return fail("null context");
+  if (!u_full || !y) return fail("cmpc_observe_step: null argument");
+  if (c->obs_plant < 0) return fail("cmpc_observe_step: call cmpc_observer_init first");
+  HIP_TRY(hipSetDevice(c->device));
+  if (observer_upload_M(c)) return -1;
+  ObserverParams P;
+  observer_params(c, &P);
+  P.y = y;
+  if (cmpc_launch_observer(P, CMPC_OBS_POST, c->stream)) return fail("observer launch failed");
+  if (check_launch("observer a-posteriori kernel")) return -1;
+  return observer_produce(c, u_full, y);
+}
+
+int cmpc_observe_apply(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  if (c->obs_plant < 0) return fail("cmpc_observe_apply: call cmpc_observer_init first");
+  if (c->lin_bound) return fail("cmpc_observe_apply: records are bound externally");
+  HIP_TRY(hipSetDevice(c->device));
+  ObserverParams P;
+  observer_params(c, &P);
+  if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream)) return fail("observer launch failed");
+  return check_launch("observer a-priori kernel");
+}
+
+int cmpc_get_observer_state(cmpc_ctx* c, double* host) {
+  if (!c || !host) return fail("null argument");
+  if (!c->obs) return fail("no observer state (cmpc_set_observer)");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(host, c->obs, sizeof(double) * (size_t)c->nqp * c->obs_len,
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int cmpc_set_observer_state(cmpc_ctx* c, const double* host) {
+  if (!c || !host) return fail("null argument");
+  if (!c->obs) return fail("no observer state (cmpc_set_observer)");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(c->obs, host, sizeof(double) * (size_t)c->nqp * c->obs_len,
+                         hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
 }
 
 // LDS layout of the build kernel (doubles; must match cmpc_kernels.hip).

@@ -91,6 +91,31 @@ struct ProduceParams {
   double p_in, p_out, Ts;
   int input_order[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS];
   int out_idx[CMPC_MAX_S_PRODUCE][4];
+  // per-QP mode (the observer's closed loop): one linearisation per QP slot
+  // q at x + q * x_stride, dx_aug row stride dx_stride, and the plant's full
+  // output matrix (n_outputs x ns) stored to c_out + q * c_stride
+  int per_qp, x_stride, dx_stride, c_stride;
+  double* c_out;
+};
+
+// Observer kernels (observer.hip)
+#define CMPC_OBS_INIT 0
+#define CMPC_OBS_POST 1
+#define CMPC_OBS_PRIOR 2
+struct ObserverParams {
+  double* obs;              // nqp * obs_len state rows
+  const double* M;          // S * nobs * n_out observer gains
+  const double* y;          // B * n_out plant outputs (init / post)
+  const double* x_init;     // B * ns (init)
+  const double* dx_init;    // nqp * ntot or null (init)
+  const double* lin;        // step records (prior: B, f)
+  const double* du_old;     // nqp * nV plans (prior)
+  double* u_old;            // nqp * nu_tot (prior)
+  int nqp, S, ns, ndist, nobs, ntot, n_out, obs_len;
+  int nu, nu_tot, nV, nd, rec_len, off_B, off_f;
+  int delay[CMPC_MAX_INPUTS];   // per input (sub-controller order)
+  int dinput[CMPC_MAX_INPUTS];  // k-th delayed input -> input index
+  int blk[CMPC_MAX_INPUTS];     // first dx index of delay block k
 };
 
 // One Jacobi iteration of the sub-controller-sharded cooperative loop
@@ -118,4 +143,5 @@ int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream);
+int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream);
 int cmpc_launch_coupled(const CoupledParams& P, int n, int nu, void* stream);

@@ -47,8 +47,11 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   __shared__ int src[CMPC_MAX_S_PRODUCE * 2 * 64 * CMPC_REC_CHUNKS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane / kLanes, l = lane - g * kLanes;  // scenario row, lane in row
-  const int b = (blockIdx.x * kWaves + wave) * kSpw + g;
-  const bool valid = b < P.B;  // (rows past the batch idle but keep the wave's syncs)
+  // unit: scenario b (S records), or in per-QP mode QP slot q (its record)
+  const int unit = (blockIdx.x * kWaves + wave) * kSpw + g;
+  const bool valid = unit < (P.per_qp ? P.B * P.S : P.B);  // (rows past the batch idle
+                                                           //  but keep the wave's syncs)
+  const int b = P.per_qp ? unit / P.S : unit;
   constexpr int ns = PLANT == CMPC_PLANT_PARALLEL ? 11 : 10;
   constexpr int ni = PLANT == CMPC_PLANT_PARALLEL ? 9 : 8;
   double* w = lds + (wave * kSpw + g) * kScnLds;
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   }
   __syncthreads();
 
-  if (valid && l < ns) xs[l] = P.x[(size_t)b * ns + l];
+  if (valid && l < ns) xs[l] = P.per_qp ? P.x[(size_t)unit * P.x_stride + l] : P.x[(size_t)b * ns + l];
   if (valid && l < ni) us[l] = P.u_full[(size_t)b * ni + l];
   for (int e = l; e < ns * ns; e += kLanes) A[e] = 0.0;  // the row clears, its lane 0
   for (int e = l; e < ns * 4; e += kLanes) {             // writes the nonzeros
@@ -140,8 +143,13 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   }
   if (!valid || PRODUCE_EXP == 3) return;
 
-  // records of the S sub-controllers of scenario b
-  for (int s = 0; s < P.S; ++s) {
+  // the observer's next a-posteriori step reads this linearisation's C
+  if (P.per_qp)
+    for (int e = l; e < P.n_outputs * ns; e += kLanes) P.c_out[(size_t)unit * P.c_stride + e] = Cc[e];
+  // records of the S sub-controllers of scenario b (per-QP mode: of slot q)
+  const int s0 = P.per_qp ? unit - b * P.S : 0, s1 = P.per_qp ? s0 + 1 : P.S;
+  const int dxs = P.per_qp ? P.dx_stride : P.naug;
+  for (int s = s0; s < s1; ++s) {
     const size_t q = (size_t)b * P.S + s;
     double* rec = P.lin + q * P.rec_len;
     const int* srow = src + s * P.rec_len;
@@ -151,7 +159,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
       if (t >= 0) v = w[t];
       else if (t == kZero) v = 0.0;
       else if (t == kOne) v = 1.0;
-      else if (t <= kDx) v = P.dx_aug ? P.dx_aug[q * P.naug + (kDx - t)] : 0.0;
+      else if (t <= kDx) v = P.dx_aug ? P.dx_aug[q * dxs + (kDx - t)] : 0.0;
       else v = P.y[(size_t)b * P.n_outputs + (kY - t)];
       rec[e] = v;
     }
@@ -162,7 +170,8 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int grid = (P.B + kWaves * kSpw - 1) / (kWaves * kSpw);
+  const int units = P.per_qp ? P.B * P.S : P.B;
+  const int grid = (units + kWaves * kSpw - 1) / (kWaves * kSpw);
   if (plant == CMPC_PLANT_PARALLEL)
     hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves), 0,
                        s, P);

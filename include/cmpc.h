@@ -212,6 +212,46 @@ int cmpc_coupled_iterate(cmpc_ctx* ctx, int S_total, int S_local, int s_offset,
                          const double* G_ext, const double* du_all, double* du_out,
                          uint32_t flags);
 
+/* Observer and receding-horizon update on the device (SURVEY.md §8(f)
+ * row 2).  Each QP slot keeps the state of its sub-controller's
+ * DistributedController (observer.h:53-56, distributed_controller.h:104-111)
+ * in HBM, a row of cmpc_observer_len() doubles:
+ *   [x_hat ns][dx_aug ntot][y_old n_outputs][C n_outputs x ns]
+ * (ntot = ns + ndist + delay states, the full AugmentedState; C = the plant
+ * output matrix of the last linearisation).  A closed-loop control step is
+ *   cmpc_observe_step(u_full, y)   ObserveAPosteriori + x_ += (observer.cc:27-44,
+ *                                  distributed_controller.cc:80), then
+ *                                  Update(x_, u_full) per QP slot: the lin
+ *                                  records (GenerateInitialQP, :75-110)
+ *   cmpc_build, cmpc_iterate(K, 0) the QP and the Jacobi iterations (no
+ *                                  CMPC_APPLY_MOVE: the update below applies it)
+ *   cmpc_observe_apply()           UpdateU (distributed_controller.h:145-152):
+ *                                  ObserveAPriori (observer.cc:8-22) with the own
+ *                                  first move (other inputs zero,
+ *                                  nerve_center.h:323-328), then u_old += du
+ * All device pointers; asynchronous on the context's stream. */
+/* ObserverMatrix M of sub-controller s ((ns + ndist) x n_outputs, row-major;
+ * the DistributedController constructor argument, distributed_controller.cc:14).
+ * n_outputs (the plant's outputs, ObserverOutputIndices) must agree for all s. */
+int cmpc_set_observer(cmpc_ctx* ctx, int s, int n_outputs, const double* M);
+int cmpc_observer_len(const cmpc_ctx* ctx);
+/* DistributedController::Initialize (distributed_controller.cc:30-43):
+ * x_hat = x_init[b] (B x ns), y_old = y_init[b] (B x n_outputs), dx_aug =
+ * dx_init (B*S x ntot, or NULL for zero), then the records at x_init (as
+ * cmpc_produce_lin, input_order / out_idx as there).  Follow with cmpc_build
+ * and cmpc_init_warmstart (InitializeQPProblem). */
+int cmpc_observer_init(cmpc_ctx* ctx, int plant, double p_in, double p_out, double Ts,
+                       const int32_t* input_order, const int32_t* out_idx,
+                       const double* x_init, const double* u_full, const double* y_init,
+                       const double* dx_init);
+/* u_full: B x n_inputs plant input at the linearisation (NerveCenter
+ * u_old_ + u_offset, nerve_center.h:139); y: B x n_outputs measured outputs. */
+int cmpc_observe_step(cmpc_ctx* ctx, const double* u_full, const double* y);
+int cmpc_observe_apply(cmpc_ctx* ctx);
+/* Host copies of the observer state rows (B*S x cmpc_observer_len()). */
+int cmpc_get_observer_state(cmpc_ctx* ctx, double* host);
+int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
+
 /* Device producer: AugmentedLinearizedSystem::Update
  * (libs/aug_lin_sys.cc:145-177, DiscretizeRK4 :232-255) for every scenario b
  * of the context's batch, on the GPU.  Linearises the plant at (x[b],

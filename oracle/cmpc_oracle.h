@@ -18,6 +18,7 @@
  *                  and the six step-0 golden records)
  *   or_nerve.c     NerveCenter Jacobi loop / DistributedController::GetInput
  *                  over a batch in the product's lin-record format
+ *   or_observer.c  Observer a posteriori / a priori and UpdateU
  *
  * The product must never route through this library.
  */
@@ -111,6 +112,20 @@ int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
             uint32_t flags, int init, int threads, double* u_old,
             double* du_old, uint32_t* ws, double* du, int32_t* status,
             int32_t* nwsr, uint8_t* trace, int32_t* ntrace);
+
+/* ---- observer (or_observer.c) ---- */
+/* ObserveAPosteriori + x_ += (libs/observer.cc:27-44,
+ * distributed_controller.cc:80).  dx: full AugmentedState (ns + ndist +
+ * delay states); Cp: n_out x ns plant C of the last linearisation;
+ * M: (ns + ndist) x n_out. */
+void or_observe_post(int ns, int ndist, int n_out, const double* Cp,
+                     const double* M, const double* y, double* y_old,
+                     double* dx, double* x_hat);
+/* UpdateU: ObserveAPriori (libs/observer.cc:8-22) with the step's record,
+ * then u_old += du (include/distributed_controller.h:145-152); du = own
+ * first move, zero for the other inputs (nerve_center.h:323-328). */
+int or_observe_prior(const cmpc_dims* d, const double* rec, const double* du_own,
+                     double* u_old, double* dx);
 
 #ifdef __cplusplus
 }

@@ -146,3 +146,51 @@ def step(dims, arrays, lin, K, u_old, du_old, ws, flags=0, init=False, threads=1
                        iptr(ntrace) if want_trace else None)
     assert rc == 0
     return du, status, nwsr, trace, ntrace
+
+
+def _observer_sigs():
+    L = lib()
+    if getattr(L, "_obs_sigs", False):
+        return L
+    P, d = ctypes.POINTER, ctypes.c_double
+    L.or_observe_post.argtypes = [ctypes.c_int] * 3 + [P(d)] * 6
+    L.or_observe_post.restype = None
+    L.or_observe_prior.argtypes = [P(CmpcDims), P(d), P(d), P(d), P(d)]
+    L.or_observe_prior.restype = ctypes.c_int
+    L._obs_sigs = True
+    return L
+
+
+def observe_post(ns, ndist, Cp, M, y, y_old, dx, x_hat):
+    """or_observe_post; y_old, dx, x_hat (float64, contiguous) updated in place."""
+    n_out = len(y)
+    Cp = np.ascontiguousarray(Cp, dtype=np.float64)
+    M = np.ascontiguousarray(M, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    for a in (y_old, dx, x_hat):
+        assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    _observer_sigs().or_observe_post(ns, ndist, n_out, dptr(Cp), dptr(M), dptr(y), dptr(y_old),
+                                     dptr(dx), dptr(x_hat))
+
+
+def observe_prior(dims, rec, du_own, u_old, dx):
+    """or_observe_prior; u_old, dx updated in place."""
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    du_own = np.ascontiguousarray(du_own, dtype=np.float64)
+    for a in (u_old, dx):
+        assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    rc = _observer_sigs().or_observe_prior(ctypes.byref(dims), dptr(rec), dptr(du_own), dptr(u_old),
+                                           dptr(dx))
+    assert rc == 0
+
+
+def plant_linearize(plant: int, x, u_full, p_in=1.0, p_out=1.0):
+    """or_plant_linearize: continuous (A, B, C, f); C is n_outputs x ns."""
+    ns, ni, no, nci = (ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
+    lib().or_plant_dims(plant, ctypes.byref(ns), ctypes.byref(ni), ctypes.byref(no), ctypes.byref(nci))
+    ns, no, nci = ns.value, no.value, nci.value
+    A, B, C, f = np.zeros(ns * ns), np.zeros(ns * nci), np.zeros(no * ns), np.zeros(ns)
+    lib().or_plant_linearize(plant, p_in, p_out, dptr(np.ascontiguousarray(x, dtype=np.float64)),
+                             dptr(np.ascontiguousarray(u_full, dtype=np.float64)), dptr(A), dptr(B),
+                             dptr(C), dptr(f))
+    return A.reshape(ns, ns), B.reshape(ns, nci), C.reshape(no, ns), f
