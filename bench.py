@@ -217,10 +217,14 @@ def main():
         # (SURVEY §8(f) row 2): a posteriori update + linearisation at each
         # slot's x_hat, build, K iterations, a priori update + u_old += du
         try:
+            # the reference's gain M is unknown (missing harness include): a
+            # disturbance-only gain [0; 0.5 I] (offset-free MPC convention);
+            # a random gain is an unstable observer (tools/closed_loop_observer.py)
             L0 = ctx.layout
-            rng_o = np.random.default_rng(79 + rank)
+            Mg = np.zeros((L0.nobs, ys.shape[1]))
+            Mg[cfg.ns:cfg.ns + cfg.ndist, :cfg.ndist] = 0.5 * np.eye(cfg.ndist)
             for s_ in range(S):
-                ctx.set_observer(s_, 0.01 * rng_o.standard_normal((L0.nobs, ys.shape[1])))
+                ctx.set_observer(s_, Mg)
             ctx.set_state(synthetic_u_old(cfg, B, np.random.default_rng(78 + rank)),
                           np.zeros((B * S, cfg.nV)), np.zeros(B * S, np.uint32))
             ctx.observer_init(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
@@ -253,7 +257,7 @@ def main():
                 "qp_solves_per_s": B * S * K / t_full,
                 "note": "observe a posteriori + per-QP linearisation at x_hat (records), build, "
                         "K iterations, observe a priori + u_old update; measured y held fixed, "
-                        f"random observer gain (0.01 scale), {reps} consecutive steps"}
+                        f"disturbance-only observer gain [0; 0.5 I], {reps} consecutive steps"}
         except Exception as e:
             log(f"observer closed-loop variant failed: {e}")
     except Exception as e:  # reported, never required

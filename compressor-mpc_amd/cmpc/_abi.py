@@ -84,6 +84,7 @@ EXPORTS = (
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
+    "cmpc_observer_init_host", "cmpc_observe_step_host",
 )
 
 _lib = None
@@ -143,6 +144,9 @@ def load_library(path: str = LIB_PATH):
                                 c_void, c_void], ctypes.c_int),
         "cmpc_observe_step": ([c_void, c_void, c_void], ctypes.c_int),
         "cmpc_observe_apply": ([c_void], ctypes.c_int),
+        "cmpc_observer_init_host": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), P(dbl),
+                                     P(dbl), P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_observe_step_host": ([c_void, P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_get_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_set_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,

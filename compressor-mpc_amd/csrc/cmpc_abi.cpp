@@ -93,6 +93,8 @@ struct cmpc_ctx {
   std::vector<int> have_M;
   bool obsM_dirty = true;
   double *d_obsM = nullptr, *obs = nullptr;
+  double* stage = nullptr;  // host-pointer observer calls: device staging
+  size_t stage_cap = 0;
   int obs_io[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS] = {};
   int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
   // timing
@@ -326,7 +328,8 @@ int cmpc_destroy(cmpc_ctx* c) {
     }
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
-                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace, c->obs, c->d_obsM};
+                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace, c->obs, c->d_obsM,
+                  c->stage};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -666,6 +669,61 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   observer_params(c, &P);
   if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream)) return fail("observer launch failed");
   return check_launch("observer a-priori kernel");
+}
+
+// copies host arrays (nullptr entries skipped) into the context's staging
+// buffer on its stream; returns their device addresses
+static int stage_host(cmpc_ctx* c, const double* const* host, const size_t* n, int k,
+                      const double** dev) {
+  size_t tot = 0;
+  for (int i = 0; i < k; ++i) tot += host[i] ? (n[i] + 1) / 2 * 2 : 0;
+  if (tot > c->stage_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->stage) HIP_TRY(hipFree(c->stage));
+    c->stage = nullptr;
+    HIP_TRY(hipMalloc(&c->stage, sizeof(double) * tot));
+    c->stage_cap = tot;
+  }
+  size_t off = 0;
+  for (int i = 0; i < k; ++i) {
+    dev[i] = nullptr;
+    if (!host[i]) continue;
+    HIP_TRY(hipMemcpyAsync(c->stage + off, host[i], sizeof(double) * n[i], hipMemcpyHostToDevice,
+                           c->stream));
+    dev[i] = c->stage + off;
+    off += (n[i] + 1) / 2 * 2;
+  }
+  return 0;
+}
+
+int cmpc_observer_init_host(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
+                            const int32_t* input_order, const int32_t* out_idx,
+                            const double* x_init, const double* u_full, const double* y_init,
+                            const double* dx_init) {
+  if (!c) return fail("null context");
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(plant, &ns, &ni, &no, &nci)) return fail("cmpc_observer_init_host: unknown plant");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t B = c->d.B;
+  const double* h[4] = {x_init, u_full, y_init, dx_init};
+  const size_t n[4] = {B * ns, B * ni, B * no, (size_t)c->nqp * c->L.ntot};
+  const double* d[4];
+  if (stage_host(c, h, n, 4, d)) return -1;
+  return cmpc_observer_init(c, plant, p_in, p_out, Ts, input_order, out_idx, d[0], d[1], d[2], d[3]);
+}
+
+int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
+  if (!c) return fail("null context");
+  if (c->obs_plant < 0) return fail("cmpc_observe_step_host: call cmpc_observer_init first");
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(c->obs_plant, &ns, &ni, &no, &nci)) return fail("unknown plant");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t B = c->d.B;
+  const double* h[2] = {u_full, y};
+  const size_t n[2] = {B * ni, B * no};
+  const double* d[2];
+  if (stage_host(c, h, n, 2, d)) return -1;
+  return cmpc_observe_step(c, d[0], d[1]);
 }
 
 int cmpc_get_observer_state(cmpc_ctx* c, double* host) {

@@ -16,9 +16,10 @@
 // C is the plant output matrix of the last linearisation (written by the
 // producer), as the reference's observer reads it through p_auglinsys_.
 //
-// One wave per QP: the record and state rows are contiguous, so the lanes'
-// loads coalesce; the few cross-lane values (dx head, the innovation, the
-// adjusted inputs) pass through LDS.  Arithmetic order, and the two exact
+// Instantiated for the two plants (ns = 11 / 10, four outputs and inputs):
+// with compile-time dims every load is issued up front and the few
+// cross-lane values (dx head, the innovation, the adjusted inputs) move by
+// lane shuffles, so a wave pays about one memory round trip.  Arithmetic order, and the two exact
 // elisions (the zero products of C's identity block and of Aorig * 0), match
 // the oracle (oracle/or_observer.c) term for term.
 #include <hip/hip_runtime.h>
@@ -50,72 +51,98 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_init_kernel(ObserverPara
   if (lane < P.n_out) st[P.ns + P.ntot + lane] = P.y[(size_t)b * P.n_out + lane];
 }
 
+// a posteriori: four QPs per wave, one 16-lane row each (nobs <= 16).  All
+// loads are issued up front (dims are compile-time), the cross-lane values
+// move by lane shuffles inside the row.
+template <int NS, int NO>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_post_kernel(ObserverParams P) {
-  __shared__ double sdx[kWaves][32];
-  __shared__ double sv[kWaves][8];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = blockIdx.x * kWaves + wave;
-  if (q >= P.nqp) return;  // (whole waves exit together)
-  const int b = q / P.S, s = q - b * P.S;
-  const int ns = P.ns, nobs = P.nobs, no = P.n_out;
-  double* st = P.obs + (size_t)q * P.obs_len;
-  double* dx = st + ns;
+  constexpr int ND = NO;  // disturbance states = outputs (C = [C_plant | I])
+  constexpr int NOBS = NS + ND;
+  static_assert(NOBS <= 16, "one 16-lane row per QP");
+  const int lane = threadIdx.x & 63;
+  const int row = lane >> 4, l = lane & 15, base = lane & ~15;
+  const int q = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4 + row;
+  const bool valid = q < P.nqp;
+  const int qq = valid ? q : P.nqp - 1;  // (idle rows read a valid slot, store nothing)
+  const int b = qq / P.S, s = qq - b * P.S;
+  double* st = P.obs + (size_t)qq * P.obs_len;
+  double* dx = st + NS;
   double* yo = dx + P.ntot;
-  const double* C = yo + no;
-  const double* y = P.y + (size_t)b * no;
-  const double* M = P.M + (size_t)s * nobs * no;
-  double dxl = 0.0;
-  if (lane < nobs) {
-    dxl = dx[lane];
-    sdx[wave][lane] = dxl;
-  }
-  WAVE_SYNC();
-  // innovation v = (y - y_old) - C dx[:nobs]   (lane o)
-  if (lane < no) {
-    double t = 0.0;
-    for (int j = 0; j < ns; ++j) t += C[lane * ns + j] * sdx[wave][j];
-    if (lane < P.ndist) t = t + sdx[wave][ns + lane];
-    sv[wave][lane] = (y[lane] - yo[lane]) - t;
-  }
-  WAVE_SYNC();
+  const double* C = yo + NO;
+  const double* y = P.y + (size_t)b * NO;
+  const double* M = P.M + (size_t)s * NOBS * NO;
+  // loads: dx[l] and M row l (lanes < nobs); C row l, y, y_old (lanes < n_out)
+  const double dxl = (l < NOBS) ? dx[l] : 0.0;
+  const double xl = (l < NS) ? st[l] : 0.0;
+  double mrow[NO], crow[NS];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) mrow[o] = (l < NOBS) ? M[l * NO + o] : 0.0;
+  const int lc = l < NO ? l : 0;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) crow[j] = C[lc * NS + j];
+  const double yl = y[lc], yol = yo[lc];
+  // innovation v = (y - y_old) - C dx[:nobs]   (lane o < n_out)
+  double t = 0.0;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) t += crow[j] * __shfl(dxl, base + j, 64);
+  t = t + __shfl(dxl, base + NS + lc, 64);
+  const double v = (yl - yol) - t;
   // dx[:nobs] += M v   (lane k);  y_old = y;  x_ += dx[:ns]
-  if (lane < nobs) {
-    double acc = 0.0;
-    for (int o = 0; o < no; ++o) acc += M[lane * no + o] * sv[wave][o];
-    dxl = dxl + acc;
-    dx[lane] = dxl;
-    if (lane < ns) st[lane] = st[lane] + dxl;
-  }
-  if (lane < no) yo[lane] = y[lane];
+  double acc = 0.0;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) acc += mrow[o] * __shfl(v, base + o, 64);
+  const double dn = dxl + acc;
+  if (!valid) return;
+  if (l < NOBS) dx[l] = dn;
+  if (l < NS) st[l] = xl + dn;
+  if (l < NO) yo[l] = yl;
 }
 
+// a priori + u_old update: one QP per wave (the delay blocks span ntot - nobs
+// entries, two per lane).  Looping several QPs per wave measured slower
+// (0.136 vs 0.111 ms for 131k QPs): the kernel is bound by load latency x
+// rounds of resident waves, so fewer waves in flight expose more of it.  Every source value is loaded before any store.
+template <int NS, int NUT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverParams P) {
-  __shared__ double sdup[kWaves][CMPC_MAX_INPUTS];
-  __shared__ double sseg[kWaves][CMPC_MAX_INPUTS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = blockIdx.x * kWaves + wave;
-  if (q >= P.nqp) return;
-  const int ns = P.ns, nobs = P.nobs, nut = P.nu_tot, nd = P.nd;
-  double* st = P.obs + (size_t)q * P.obs_len;
-  double* dx = st + ns;
-  const double* rec = P.lin + (size_t)q * P.rec_len;
-  double* uo = P.u_old + (size_t)q * nut;
-  // du = own first move (others zero, nerve_center.h:323-328);
-  // du' = du + u_old on delayed inputs (AdjustAppliedInput)
-  double du = 0.0, u0 = 0.0;
-  if (lane < nut) {
-    u0 = uo[lane];
-    du = (lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0;
-    double dup = du;
-    if (P.delay[lane]) dup += u0;
-    sdup[wave][lane] = dup;
+  const int lane = threadIdx.x & 63;
+  const int nobs = P.nobs, nd = P.nd;
+  // delay tables in registers (compile-time indices: a runtime-indexed
+  // kernel-argument read is a dependent memory load)
+  int dl[NUT], din[NUT], blk[NUT];
+#pragma unroll
+  for (int i = 0; i < NUT; ++i) {
+    dl[i] = P.delay[i];
+    din[i] = P.dinput[i];
+    blk[i] = P.blk[i];
   }
-  // dx' delayed-input slots minus u_old (AdjustFirstDelayedStates)
-  if (lane < nd) sseg[wave][lane] = dx[nobs + lane] - uo[P.dinput[lane]];
-  // aug part (delayed-input slots and delay blocks), two elements per lane:
-  // slot k <- first state of block k; a block state <- its successor; the
-  // block's last state <- du' of its input (Baug).  Sources are loaded
-  // before any store.
+  auto pick = [](const int* a, int k) {
+    int v = a[0];
+#pragma unroll
+    for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
+    return v;
+  };
+  const int q = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (q >= P.nqp) return;  // (whole waves exit together)
+  double* st = P.obs + (size_t)q * P.obs_len;
+  double* dx = st + NS;
+  const double* rec = P.lin + (size_t)q * P.rec_len;
+  double* uo = P.u_old + (size_t)q * NUT;
+  // lanes < nu_tot: u_old, du = own first move (others zero, nerve_center.h:323-328)
+  const int li = lane < NUT ? lane : 0;
+  const double u0 = uo[li];
+  const double du = (lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0;
+  // lanes < nd: delayed-input slot value and its input's u_old
+  const int lk = lane < nd ? lane : 0;
+  const double slot = dx[nobs + lk];
+  const double useg = uo[pick(din, lk)];
+  // lanes < ns: row of B (sub-controller input order) and f
+  const int ls = lane < NS ? lane : 0;
+  double brow[NUT];
+#pragma unroll
+  for (int i = 0; i < NUT; ++i) brow[i] = rec[P.off_B + ls * NUT + i];
+  const double fl = rec[P.off_f + ls];
+  // aug part, two entries per lane: slot k <- first state of block k; a block
+  // state <- its successor; the block's last state <- du' of its input (Baug)
   double nv[2];
   int tgt[2], from_du[2];
 #pragma unroll
@@ -127,32 +154,52 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     if (e < P.ntot) {
       tgt[h] = e;
       if (e < nobs + nd) {
-        nv[h] = dx[P.blk[e - nobs]];
+        nv[h] = dx[pick(blk, e - nobs)];
       } else {
         int k = 0;
-        while (k + 1 < nd && e >= P.blk[k + 1]) ++k;
-        const int i = P.dinput[k];
-        if (e - P.blk[k] < P.delay[i] - 2) nv[h] = dx[e + 1];
+#pragma unroll
+        for (int kk = 1; kk < NUT; ++kk) k += (kk < nd && e >= blk[kk]) ? 1 : 0;
+        const int i = pick(din, k);
+        if (e - pick(blk, k) < pick(dl, i) - 2) nv[h] = dx[e + 1];
         else from_du[h] = i;
       }
     }
   }
-  WAVE_SYNC();
-  // states: (B du')[:ns] + (Adelay seg) + f
-  if (lane < ns) {
-    const double* Br = rec + P.off_B + lane * nut;
-    double bsum = 0.0;
-    for (int i = 0; i < nut; ++i)
-      if (!P.delay[i]) bsum += Br[i] * sdup[wave][i];
-    double t = 0.0;
-    for (int k = 0; k < nd; ++k) t += Br[P.dinput[k]] * sseg[wave][k];
-    dx[lane] = (bsum + t) + rec[P.off_f + lane];
-  }
+  // du' = du + u_old on delayed inputs (AdjustAppliedInput); dx' slots minus
+  // u_old (AdjustFirstDelayedStates)
+  const double dup = pick(dl, li) ? du + u0 : du;
+  const double seg = slot - useg;
+  double dupv[NUT];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (tgt[h] >= 0) dx[tgt[h]] = from_du[h] >= 0 ? sdup[wave][from_du[h]] : nv[h];
+  for (int i = 0; i < NUT; ++i) dupv[i] = __shfl(dup, i, 64);
+  // states: (B du')[:ns] + (Adelay seg) + f
+  double bsum = 0.0;
+#pragma unroll
+  for (int i = 0; i < NUT; ++i)
+    if (!dl[i]) bsum += brow[i] * dupv[i];
+  double tsum = 0.0;
+#pragma unroll
+  for (int k = 0; k < NUT; ++k) {
+    const double sk = __shfl(seg, k, 64);
+    double bk = brow[0];
+#pragma unroll
+    for (int i = 1; i < NUT; ++i) bk = (din[k] == i) ? brow[i] : bk;
+    if (k < nd) tsum += bk * sk;
+  }
+  const double xn = (bsum + tsum) + fl;
+  WAVE_SYNC();  // all loads above have completed before the first store
+  if (lane < NS) dx[lane] = xn;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (tgt[h] < 0) continue;
+    double val = nv[h];
+#pragma unroll
+    for (int i = 0; i < NUT; ++i)
+      if (from_du[h] == i) val = dupv[i];
+    dx[tgt[h]] = val;
+  }
   // UpdateU: u_old += du (own inputs; the others add zero)
-  if (lane < nut) uo[lane] = u0 + du;
+  if (lane < NUT) uo[lane] = u0 + du;
 }
 
 }  // namespace
@@ -165,12 +212,26 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
     case CMPC_OBS_INIT:
       hipLaunchKernelGGL(cmpc_obs_init_kernel, dim3(grid), dim3(64 * kWaves), 0, s, P);
       return 0;
-    case CMPC_OBS_POST:
-      hipLaunchKernelGGL(cmpc_obs_post_kernel, dim3(grid), dim3(64 * kWaves), 0, s, P);
+    case CMPC_OBS_POST: {
+      const int g4 = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
+      if (P.ns == 11 && P.n_out == 4 && P.ndist == 4)
+        hipLaunchKernelGGL((cmpc_obs_post_kernel<11, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
+      else if (P.ns == 10 && P.n_out == 4 && P.ndist == 4)
+        hipLaunchKernelGGL((cmpc_obs_post_kernel<10, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
+      else
+        return -1;
       return 0;
-    case CMPC_OBS_PRIOR:
-      hipLaunchKernelGGL(cmpc_obs_prior_kernel, dim3(grid), dim3(64 * kWaves), 0, s, P);
+    }
+    case CMPC_OBS_PRIOR: {
+      const int g8 = grid;  // one QP per wave
+      if (P.ns == 11 && P.nu_tot == 4)
+        hipLaunchKernelGGL((cmpc_obs_prior_kernel<11, 4>), dim3(g8), dim3(64 * kWaves), 0, s, P);
+      else if (P.ns == 10 && P.nu_tot == 4)
+        hipLaunchKernelGGL((cmpc_obs_prior_kernel<10, 4>), dim3(g8), dim3(64 * kWaves), 0, s, P);
+      else
+        return -1;
       return 0;
+    }
   }
   return -1;
 }

@@ -248,6 +248,13 @@ int cmpc_observer_init(cmpc_ctx* ctx, int plant, double p_in, double p_out, doub
  * u_old_ + u_offset, nerve_center.h:139); y: B x n_outputs measured outputs. */
 int cmpc_observe_step(cmpc_ctx* ctx, const double* u_full, const double* y);
 int cmpc_observe_apply(cmpc_ctx* ctx);
+/* The same two calls with HOST arrays (staged to the device on the
+ * context's stream), for host-side harnesses such as the C++ adapter. */
+int cmpc_observer_init_host(cmpc_ctx* ctx, int plant, double p_in, double p_out, double Ts,
+                            const int32_t* input_order, const int32_t* out_idx,
+                            const double* x_init, const double* u_full, const double* y_init,
+                            const double* dx_init);
+int cmpc_observe_step_host(cmpc_ctx* ctx, const double* u_full, const double* y);
 /* Host copies of the observer state rows (B*S x cmpc_observer_len()). */
 int cmpc_get_observer_state(cmpc_ctx* ctx, double* host);
 int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);

@@ -15,15 +15,18 @@
 //   InputConstraints<nu> (per sub-controller ctor arg) include/input_constraints.h:12-26
 //   read_files.h setup-file reader                    include/read_files.h:13-81
 //
-// One difference of substance: the reference's GetNextInput runs each
-// sub-controller's observer (Observer::ObserveAPosteriori, observer.cc:6-40)
-// before linearising.  The observer gain lives in the reference's missing
-// harness include (common-simulation.inc) and the observer is outside this
-// path, so GetNextInput takes the state estimate (x_hat and
-// the augmented-state tail) from the caller.  Everything from the
-// linearisation onwards — AugmentedLinearizedSystem::Update, condensation, QP
-// build, K Jacobi iterations, UpdateUOld/SendUHelper — runs here: the
-// linearisation on the host (cmpc_plant_lin_record), the rest on the GPU.
+// Two ways to run a step:
+//  - with the observer (the reference's own pattern): SetObserver(s, M) for
+//    every sub-controller (M is the DistributedController constructor
+//    argument, distributed_controller.cc:14), then Initialize(...) and
+//    GetNextInput(y) / GetNextInputWithTiming(y, n, t) exactly as the
+//    reference.  Each sub-controller's observer (observer.cc:6-40), its
+//    linearisation at its own estimate, the QP build, K Jacobi iterations and
+//    UpdateU run on the GPU, the state estimates resident in device memory.
+//  - with an external estimate: GetNextInput(y, x_hat, dx_aug) takes the state
+//    estimate from the caller (the reference harness's gain M lives in its
+//    missing common-simulation.inc); the linearisation runs on the host
+//    (cmpc_plant_lin_record), the rest on the GPU.
 #pragma once
 
 #include <chrono>
@@ -243,9 +246,26 @@ class NerveCenter {
           "cmpc_set_constraints");
   }
 
+  /// ObserverMatrix of sub-controller s, (ns + ndist) x n_outputs row-major
+  /// (the DistributedController constructor argument).  Once set for every
+  /// sub-controller, the observer runs on the device (see the header note).
+  void SetObserver(int s, const double* M) {
+    Check(cmpc_set_observer(ctx_, s, spec_.n_outputs, M), "cmpc_set_observer");
+    if (has_M_.empty()) has_M_.assign(spec_.S(), 0);
+    has_M_[s] = 1;
+  }
+  bool observer_on() const {
+    if (has_M_.empty()) return false;
+    for (int v : has_M_)
+      if (!v) return false;
+    return true;
+  }
+
   /// Initialize(x_init, u_init, u_init_full, y_init, dx_init): linearise at
   /// (x_init, u_init_full), build every sub-controller's QP and run the cold
   /// InitializeQPProblem solve (its working sets warm-start step 0).
+  /// dx_init: the augmented-state tail (naug) without the observer, the full
+  /// AugmentedState (ns + naug) with it (distributed_controller.cc:30-43).
   void Initialize(const double* x_init, const double* u_init, const double* u_init_full,
                   const double* y_init, const double* dx_init = nullptr) {
     u_offset_.assign(u_init_full, u_init_full + spec_.n_inputs);
@@ -257,11 +277,48 @@ class NerveCenter {
     std::vector<double> du(static_cast<size_t>(spec_.S()) * spec_.nV(), 0.0);
     std::vector<uint32_t> ws(spec_.S(), 0u);
     Check(cmpc_set_state(ctx_, u_sub.data(), du.data(), ws.data()), "cmpc_set_state");
-    FillRecords(x_init, u_init_full, dx_init, y_init);
-    Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
+    if (observer_on()) {
+      std::vector<int32_t> io, oi;
+      for (int s = 0; s < spec_.S(); ++s) {
+        io.insert(io.end(), spec_.input_order[s].begin(), spec_.input_order[s].end());
+        oi.insert(oi.end(), spec_.out_idx[s].begin(), spec_.out_idx[s].end());
+      }
+      std::vector<double> dx;
+      if (dx_init)
+        for (int s = 0; s < spec_.S(); ++s) dx.insert(dx.end(), dx_init, dx_init + L_.ntot);
+      Check(cmpc_observer_init_host(ctx_, static_cast<int>(spec_.plant), 1.0, 1.0, 0.05, io.data(),
+                                    oi.data(), x_init, u_init_full, y_init,
+                                    dx_init ? dx.data() : nullptr),
+            "cmpc_observer_init_host");
+    } else {
+      FillRecords(x_init, u_init_full, dx_init, y_init);
+      Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
+    }
     Check(cmpc_build(ctx_), "cmpc_build");
     Check(cmpc_init_warmstart(ctx_), "cmpc_init_warmstart");
     Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
+  }
+
+  /// ControllerInterface::GetNextInput(y) (controller_interface.h:46), the
+  /// observer on the device (SetObserver).
+  std::vector<double> GetNextInput(const double* y) { return GetNextInputWithTiming(y, -1, nullptr); }
+
+  /// NerveCenter::GetNextInputWithTiming(y, n_timing_iterations, time_out)
+  /// (nerve_center.h:134-182), the observer on the device.
+  std::vector<double> GetNextInputWithTiming(const double* y, int n_timing_iterations,
+                                             int64_t* time_out_ns = nullptr) {
+    if (!observer_on()) throw Error("GetNextInput(y) needs SetObserver for every sub-controller");
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> u_full(u_offset_);
+    for (int c = 0; c < spec_.nu_tot; ++c) u_full[spec_.plant_input_index[c]] += u_old_[c];
+    // ObserveAPosteriori + Update at each sub-controller's estimate
+    Check(cmpc_observe_step_host(ctx_, u_full.data(), y), "cmpc_observe_step_host");
+    Check(cmpc_build(ctx_), "cmpc_build");
+    const int64_t timed = Iterate(n_timing_iterations, 0u, t0);
+    Download();
+    // UpdateU of every sub-controller (observer a priori + its u_old_)
+    Check(cmpc_observe_apply(ctx_), "cmpc_observe_apply");
+    return Finish(timed, t0, time_out_ns);
   }
 
   /// ControllerInterface::GetNextInput with the observer's estimate supplied.
@@ -284,21 +341,42 @@ class NerveCenter {
     FillRecords(x_hat, u_full.data(), dx_aug, y);
     Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
     Check(cmpc_build(ctx_), "cmpc_build");
+    const int64_t timed = Iterate(n_timing_iterations, CMPC_APPLY_MOVE, t0);
+    Download();
+    return Finish(timed, t0, time_out_ns);
+  }
+
+  /// Move plans (S x nV), QP status words and working-set change counts of the last step.
+  const std::vector<double>& last_plans() const { return du_; }
+  const std::vector<int32_t>& last_status() const { return status_; }
+  const std::vector<int32_t>& last_nwsr() const { return nwsr_; }
+
+ private:
+  // K Jacobi iterations, the last with `last_flags`; if 0 <= n < K, the wall
+  // time up to iteration n is returned (the reference's stopped cpu_timer)
+  int64_t Iterate(int n_timing_iterations, uint32_t last_flags,
+                  std::chrono::steady_clock::time_point t0) {
     int64_t timed = -1;
     if (n_timing_iterations >= 0 && n_timing_iterations < K_) {
       Check(cmpc_iterate(ctx_, n_timing_iterations, 0u), "cmpc_iterate");
       Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
       timed = std::chrono::duration_cast<std::chrono::nanoseconds>(
                   std::chrono::steady_clock::now() - t0).count();
-      Check(cmpc_iterate(ctx_, K_ - n_timing_iterations, CMPC_APPLY_MOVE), "cmpc_iterate");
+      Check(cmpc_iterate(ctx_, K_ - n_timing_iterations, last_flags), "cmpc_iterate");
     } else {
-      Check(cmpc_iterate(ctx_, K_, CMPC_APPLY_MOVE), "cmpc_iterate");
+      Check(cmpc_iterate(ctx_, K_, last_flags), "cmpc_iterate");
     }
+    return timed;
+  }
+  void Download() {
     du_.resize(static_cast<size_t>(spec_.S()) * spec_.nV());
     status_.resize(spec_.S());
     nwsr_.resize(spec_.S());
     Check(cmpc_download(ctx_, du_.data(), status_.data(), nwsr_.data()), "cmpc_download");
-    // UpdateUOld (include/nerve_center.h:313-319): apply each first move
+  }
+  // UpdateUOld (include/nerve_center.h:313-319): apply each first move
+  std::vector<double> Finish(int64_t timed, std::chrono::steady_clock::time_point t0,
+                             int64_t* time_out_ns) {
     for (int s = 0; s < spec_.S(); ++s)
       for (int c = 0; c < spec_.nu; ++c) u_old_[spec_.input_order[s][c]] += du_[s * spec_.nV() + c];
     if (time_out_ns)
@@ -308,12 +386,6 @@ class NerveCenter {
     return u_old_;
   }
 
-  /// Move plans (S x nV), QP status words and working-set change counts of the last step.
-  const std::vector<double>& last_plans() const { return du_; }
-  const std::vector<int32_t>& last_status() const { return status_; }
-  const std::vector<int32_t>& last_nwsr() const { return nwsr_; }
-
- private:
   // AugmentedLinearizedSystem::Update + observer state tail + y_prev for every
   // sub-controller (the inputs GenerateInitialQP reads).
   void FillRecords(const double* x, const double* u_full, const double* dx_aug, const double* y) {
@@ -334,6 +406,7 @@ class NerveCenter {
   cmpc_ctx* ctx_ = nullptr;
   std::vector<double> u_old_, u_offset_, rec_, du_;
   std::vector<int32_t> status_, nwsr_;
+  std::vector<int> has_M_;
 };
 
 }  // namespace cmpc

@@ -5,7 +5,9 @@
 // GetNextInputWithTiming.  Prints the applied control input u(t = 0) with 6
 // significant digits (the precision of the reference's results/*.dat).
 //
-// usage: nerve_center_step0 <setup-file> <par|ser> <cent|coop|ncoop> [p]
+// usage: nerve_center_step0 <setup-file> <par|ser> <cent|coop|ncoop> [p] [observer]
+// "observer": SetObserver for every sub-controller (an arbitrary gain: the
+// t = 0 correction is zero) and the reference's GetNextInputWithTiming(y, n, t).
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -27,7 +29,14 @@ int main(int argc, char** argv) {
     const ControllerSpec spec = ControllerSpec::Reference(plant, type, p);
     const SetupFile setup = SetupFile::Read(argv[1]);
 
+    const bool observer = argc > 5 && std::strcmp(argv[5], "observer") == 0;
     NerveCenter nc(spec, setup.n_iterations);
+    if (observer) {
+      const int nobs = spec.ns + spec.ndist;
+      std::vector<double> M(static_cast<size_t>(nobs) * spec.n_outputs, 0.0);
+      for (int o = 0; o < spec.ndist && o < spec.n_outputs; ++o) M[(spec.ns + o) * spec.n_outputs + o] = 0.5;
+      for (int s = 0; s < spec.S(); ++s) nc.SetObserver(s, M.data());
+    }
     // weights: uwt is n_control_inputs^2; ywt one ny x ny block per sub-controller
     const int blk = spec.ny * spec.ny;
     std::vector<const double*> ywt(spec.S());
@@ -59,8 +68,10 @@ int main(int argc, char** argv) {
     nc.Initialize(x0.data(), u0.data(), u_full.data(), y0.data());
     int64_t ns_time = 0;
     // t = 0: the observer's a-posteriori correction is zero, x_hat = x0
-    const std::vector<double> u = nc.GetNextInputWithTiming(y0.data(), x0.data(), nullptr,
-                                                            setup.n_timing_iterations, &ns_time);
+    const std::vector<double> u =
+        observer ? nc.GetNextInputWithTiming(y0.data(), setup.n_timing_iterations, &ns_time)
+                 : nc.GetNextInputWithTiming(y0.data(), x0.data(), nullptr,
+                                             setup.n_timing_iterations, &ns_time);
     for (int c = 0; c < spec.nu_tot; ++c) std::printf("%s%.6g", c ? " " : "", u[c]);
     std::printf("\n");
     std::fprintf(stderr, "status:");
