@@ -85,6 +85,10 @@ EXPORTS = (
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
     "cmpc_observer_init_host", "cmpc_observe_step_host",
+    "cmpc_sim_create", "cmpc_sim_destroy", "cmpc_sim_set_stream", "cmpc_sim_reset",
+    "cmpc_sim_set_input", "cmpc_sim_plant_input", "cmpc_sim_integrate", "cmpc_sim_output",
+    "cmpc_sim_synchronize", "cmpc_sim_state", "cmpc_sim_input", "cmpc_sim_step_size",
+    "cmpc_sim_status", "cmpc_accumulate_moves", "cmpc_sim_download",
 )
 
 _lib = None
@@ -147,6 +151,22 @@ def load_library(path: str = LIB_PATH):
         "cmpc_observer_init_host": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), P(dbl),
                                      P(dbl), P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_observe_step_host": ([c_void, P(dbl), P(dbl)], ctypes.c_int),
+        "cmpc_sim_create": ([P(c_void), ctypes.c_int, ctypes.c_int, ctypes.c_int, dbl, dbl,
+                             ctypes.c_int, P(i32), P(i32)], ctypes.c_int),
+        "cmpc_sim_destroy": ([c_void], ctypes.c_int),
+        "cmpc_sim_set_stream": ([c_void, c_void], ctypes.c_int),
+        "cmpc_sim_reset": ([c_void, c_void, c_void, dbl], ctypes.c_int),
+        "cmpc_sim_set_input": ([c_void, c_void], ctypes.c_int),
+        "cmpc_sim_plant_input": ([c_void, c_void, c_void], ctypes.c_int),
+        "cmpc_sim_integrate": ([c_void, dbl, dbl, dbl, dbl], ctypes.c_int),
+        "cmpc_sim_output": ([c_void, c_void], ctypes.c_int),
+        "cmpc_sim_synchronize": ([c_void], ctypes.c_int),
+        "cmpc_sim_download": ([c_void, P(dbl), P(dbl), P(dbl), P(i32)], ctypes.c_int),
+        "cmpc_sim_state": ([c_void], c_void),
+        "cmpc_sim_input": ([c_void], c_void),
+        "cmpc_sim_step_size": ([c_void], c_void),
+        "cmpc_sim_status": ([c_void], c_void),
+        "cmpc_accumulate_moves": ([c_void, P(i32), c_void], ctypes.c_int),
         "cmpc_get_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_set_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,

@@ -726,6 +726,236 @@ int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
   return cmpc_observe_step(c, d[0], d[1]);
 }
 
+// ---- plant simulation ----
+struct cmpc_sim {
+  int plant = 0, B = 0, device = 0, ns = 0, ni = 0, no = 0, nc = 0, ring_len = 0;
+  double p_in = 1.0, p_out = 1.0;
+  int delay[CMPC_MAX_INPUTS] = {}, cidx[CMPC_MAX_INPUTS] = {};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  double *x = nullptr, *dt = nullptr, *u_full = nullptr, *u_offset = nullptr, *ring = nullptr,
+         *scratch = nullptr;
+  int32_t *cur = nullptr, *status = nullptr;
+};
+
+int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, double p_out,
+                    int n_control, const int32_t* delays, const int32_t* control_index) {
+  if (!out || !delays || !control_index) return fail("null argument");
+  *out = nullptr;
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(plant, &ns, &ni, &no, &nci)) return fail("cmpc_sim_create: unknown plant");
+  if (B < 1 || B > (1 << 28)) return fail("cmpc_sim_create: bad batch");
+  if (n_control < 1 || n_control > CMPC_MAX_INPUTS) return fail("cmpc_sim_create: bad n_control");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail("no such HIP device");
+  cmpc_sim* m = new cmpc_sim();
+  m->plant = plant; m->B = B; m->device = device; m->ns = ns; m->ni = ni; m->no = no;
+  m->nc = n_control; m->p_in = p_in; m->p_out = p_out;
+  for (int i = 0; i < n_control; ++i) {
+    if (delays[i] < 0 || control_index[i] < 0 || control_index[i] >= ni) {
+      delete m;
+      return fail("cmpc_sim_create: bad delay or control index");
+    }
+    m->delay[i] = delays[i];
+    m->cidx[i] = control_index[i];
+    m->ring_len += delays[i];
+  }
+  if (m->ring_len == 0) m->ring_len = 1;
+  auto bail = [&](hipError_t e) {
+    (void)e;
+    void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->cur, m->status};
+    for (void* b : bufs)
+      if (b) (void)hipFree(b);
+    delete m;
+    return fail("cmpc_sim_create: device allocation failed");
+  };
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return bail(e);
+  if ((e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e);
+  m->own_stream = true;
+  const size_t Bz = (size_t)B;
+  if ((e = hipMalloc(&m->x, sizeof(double) * Bz * ns)) != hipSuccess ||
+      (e = hipMalloc(&m->dt, sizeof(double) * Bz)) != hipSuccess ||
+      (e = hipMalloc(&m->u_full, sizeof(double) * Bz * ni)) != hipSuccess ||
+      (e = hipMalloc(&m->u_offset, sizeof(double) * Bz * ni)) != hipSuccess ||
+      (e = hipMalloc(&m->ring, sizeof(double) * Bz * m->ring_len)) != hipSuccess ||
+      (e = hipMalloc(&m->scratch, sizeof(double) * Bz * (ni > n_control ? ni : n_control))) != hipSuccess ||
+      (e = hipMalloc(&m->cur, sizeof(int32_t) * Bz * n_control)) != hipSuccess ||
+      (e = hipMalloc(&m->status, sizeof(int32_t) * Bz)) != hipSuccess)
+    return bail(e);
+  *out = m;
+  return 0;
+}
+
+int cmpc_sim_destroy(cmpc_sim* m) {
+  if (!m) return 0;
+  (void)hipSetDevice(m->device);
+  if (m->stream) (void)hipStreamSynchronize(m->stream);
+  void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->cur, m->status};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (m->own_stream && m->stream) (void)hipStreamDestroy(m->stream);
+  delete m;
+  return 0;
+}
+
+int cmpc_sim_set_stream(cmpc_sim* m, void* stream) {
+  if (!m) return fail("null simulator");
+  HIP_TRY(hipSetDevice(m->device));
+  HIP_TRY(hipStreamSynchronize(m->stream));
+  if (m->own_stream) (void)hipStreamDestroy(m->stream);
+  m->stream = (hipStream_t)stream;
+  m->own_stream = false;
+  return 0;
+}
+
+static SimInputParams sim_input_params(cmpc_sim* m, const double* u_control, int use_delay) {
+  SimInputParams P;
+  std::memset(&P, 0, sizeof P);
+  P.u_control = u_control;
+  P.u_offset = m->u_offset;
+  P.u_full = m->u_full;
+  P.ring = m->ring;
+  P.cur = m->cur;
+  P.B = m->B;
+  P.nc = m->nc;
+  P.ni = m->ni;
+  P.ring_len = m->ring_len;
+  P.use_delay = use_delay;
+  for (int i = 0; i < m->nc; ++i) {
+    P.delay[i] = m->delay[i];
+    P.cidx[i] = m->cidx[i];
+  }
+  return P;
+}
+
+int cmpc_sim_reset(cmpc_sim* m, const double* x0, const double* u_offset, double dt0) {
+  if (!m || !x0 || !u_offset) return fail("null argument");
+  if (!(dt0 > 0)) return fail("cmpc_sim_reset: dt0 must be positive");
+  HIP_TRY(hipSetDevice(m->device));
+  const size_t Bz = (size_t)m->B;
+  HIP_TRY(hipMemcpyAsync(m->x, x0, sizeof(double) * Bz * m->ns, hipMemcpyDeviceToDevice, m->stream));
+  HIP_TRY(hipMemcpyAsync(m->u_offset, u_offset, sizeof(double) * Bz * m->ni, hipMemcpyDeviceToDevice,
+                         m->stream));
+  std::vector<double> dts(Bz, dt0);
+  HIP_TRY(hipMemcpyAsync(m->dt, dts.data(), sizeof(double) * Bz, hipMemcpyHostToDevice, m->stream));
+  // TimeDelay(): zero memory, cursor of input i at the sum of the delays before it
+  HIP_TRY(hipMemsetAsync(m->ring, 0, sizeof(double) * Bz * m->ring_len, m->stream));
+  std::vector<int32_t> cur(Bz * m->nc);
+  for (size_t b = 0; b < Bz; ++b) {
+    int sum = 0;
+    for (int i = 0; i < m->nc; ++i) {
+      cur[b * m->nc + i] = sum;
+      sum += m->delay[i];
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(m->cur, cur.data(), sizeof(int32_t) * cur.size(), hipMemcpyHostToDevice, m->stream));
+  // u_ = GetPlantInput(u_init = 0) = u_offset
+  HIP_TRY(hipMemcpyAsync(m->u_full, u_offset, sizeof(double) * Bz * m->ni, hipMemcpyDeviceToDevice,
+                         m->stream));
+  HIP_TRY(hipStreamSynchronize(m->stream));  // (host staging buffers above)
+  return 0;
+}
+
+int cmpc_sim_set_input(cmpc_sim* m, const double* u_control) {
+  if (!m || !u_control) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  const SimInputParams P = sim_input_params(m, u_control, 1);
+  if (cmpc_launch_sim_input(P, m->stream)) return fail("sim input launch failed");
+  return check_launch("sim input kernel");
+}
+
+int cmpc_sim_plant_input(cmpc_sim* m, const double* u_control, double* u_full_out) {
+  if (!m || !u_control || !u_full_out) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  SimInputParams P = sim_input_params(m, u_control, 0);
+  P.u_full = u_full_out;
+  if (cmpc_launch_sim_input(P, m->stream)) return fail("sim input launch failed");
+  return check_launch("sim input kernel");
+}
+
+int cmpc_sim_integrate(cmpc_sim* m, double t, double t_end, double eps_abs, double eps_rel) {
+  if (!m) return fail("null simulator");
+  if (!(t_end >= t)) return fail("cmpc_sim_integrate: t_end < t");
+  HIP_TRY(hipSetDevice(m->device));
+  SimParams P;
+  std::memset(&P, 0, sizeof P);
+  P.x = m->x;
+  P.dt = m->dt;
+  P.u_full = m->u_full;
+  P.status = m->status;
+  P.B = m->B;
+  P.t = t;
+  P.t_end = t_end;
+  P.eps_abs = eps_abs;
+  P.eps_rel = eps_rel;
+  P.p_in = m->p_in;
+  P.p_out = m->p_out;
+  if (cmpc_launch_sim(P, m->plant, m->stream)) return fail("sim launch failed");
+  return check_launch("sim kernel");
+}
+
+int cmpc_sim_output(cmpc_sim* m, double* y) {
+  if (!m || !y) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  if (cmpc_launch_sim_output(m->plant, m->x, y, m->B, m->stream)) return fail("sim output launch failed");
+  return check_launch("sim output kernel");
+}
+
+int cmpc_sim_download(cmpc_sim* m, double* x, double* u_full, double* dt, int32_t* status) {
+  if (!m) return fail("null simulator");
+  HIP_TRY(hipSetDevice(m->device));
+  const size_t Bz = (size_t)m->B;
+  if (x) HIP_TRY(hipMemcpyAsync(x, m->x, sizeof(double) * Bz * m->ns, hipMemcpyDeviceToHost, m->stream));
+  if (u_full)
+    HIP_TRY(hipMemcpyAsync(u_full, m->u_full, sizeof(double) * Bz * m->ni, hipMemcpyDeviceToHost, m->stream));
+  if (dt) HIP_TRY(hipMemcpyAsync(dt, m->dt, sizeof(double) * Bz, hipMemcpyDeviceToHost, m->stream));
+  if (status)
+    HIP_TRY(hipMemcpyAsync(status, m->status, sizeof(int32_t) * Bz, hipMemcpyDeviceToHost, m->stream));
+  HIP_TRY(hipStreamSynchronize(m->stream));
+  return 0;
+}
+
+double* cmpc_sim_state(cmpc_sim* m) { return m ? m->x : nullptr; }
+double* cmpc_sim_input(cmpc_sim* m) { return m ? m->u_full : nullptr; }
+double* cmpc_sim_step_size(cmpc_sim* m) { return m ? m->dt : nullptr; }
+int32_t* cmpc_sim_status(cmpc_sim* m) { return m ? m->status : nullptr; }
+
+int cmpc_sim_synchronize(cmpc_sim* m) {
+  if (!m) return fail("null simulator");
+  HIP_TRY(hipSetDevice(m->device));
+  HIP_TRY(hipStreamSynchronize(m->stream));
+  return 0;
+}
+
+// NerveCenter::UpdateUOld at the nerve level (nerve_center.h:313-319): the
+// control input u_old_ (B x nu_tot, plant control order) += every
+// sub-controller's first move of its own inputs (ControlInputIndices order)
+int cmpc_accumulate_moves(cmpc_ctx* c, const int32_t* input_order, double* u_control) {
+  if (!c || !input_order || !u_control) return fail("null argument");
+  const cmpc_dims& d = c->d;
+  if (d.S > CMPC_MAX_S_PRODUCE) return fail("cmpc_accumulate_moves: too many sub-controllers");
+  AccumParams P;
+  std::memset(&P, 0, sizeof P);
+  P.du = c->du_old;
+  P.u_control = u_control;
+  P.B = d.B;
+  P.S = d.S;
+  P.nu = d.nu;
+  P.nu_tot = d.nu_tot;
+  P.nV = c->L.nV;
+  for (int s = 0; s < d.S; ++s)
+    for (int k = 0; k < d.nu; ++k) {
+      const int v = input_order[s * d.nu_tot + k];
+      if (v < 0 || v >= d.nu_tot) return fail("cmpc_accumulate_moves: bad input_order");
+      P.order[s][k] = v;
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  if (cmpc_launch_accumulate(P, c->stream)) return fail("accumulate launch failed");
+  return check_launch("accumulate kernel");
+}
+
 int cmpc_get_observer_state(cmpc_ctx* c, double* host) {
   if (!c || !host) return fail("null argument");
   if (!c->obs) return fail("no observer state (cmpc_set_observer)");

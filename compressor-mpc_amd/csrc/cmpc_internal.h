@@ -142,6 +142,36 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
+// Plant simulation (sim.hip)
+struct SimParams {
+  double* x;              // B * ns
+  double* dt;             // B (controlled stepper's step, carried between intervals)
+  const double* u_full;   // B * n_inputs
+  int32_t* status;        // B or null (1: step-size control failed)
+  int B;
+  double t, t_end, eps_abs, eps_rel, p_in, p_out;
+};
+struct SimInputParams {
+  const double* u_control;  // B * nc
+  const double* u_offset;   // B * ni
+  double* u_full;           // B * ni
+  double* ring;             // B * ring_len
+  int32_t* cur;             // B * nc
+  int B, nc, ni, ring_len, use_delay;
+  int delay[CMPC_MAX_INPUTS];
+  int cidx[CMPC_MAX_INPUTS];
+};
+struct AccumParams {
+  const double* du;   // nqp * nV
+  double* u_control;  // B * nu_tot
+  int B, S, nu, nu_tot, nV;
+  int order[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS];
+};
+int cmpc_launch_accumulate(const AccumParams& P, void* stream);
+int cmpc_launch_sim(const SimParams& P, int plant, void* stream);
+int cmpc_launch_sim_input(const SimInputParams& P, void* stream);
+int cmpc_launch_sim_output(int plant, const double* x, double* y, int B, void* stream);
+
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream);
 int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream);
 int cmpc_launch_coupled(const CoupledParams& P, int n, int nu, void* stream);

@@ -193,6 +193,38 @@ CMPC_PHD void parallel_linearize(double p_in, double p_out, const double* x, con
   f[10] = kC2 / tank.volume * (flow_total - valve_flow(x[10], p_out, u[8], tank.D, tank.m_out_c)) * 1e-5;
 }
 
+// ParallelCompressors::GetDerivative (systems/parallel_compressors.cc:9-26;
+// tank: systems/tank.cc:10-24)
+CMPC_PHD void parallel_derivative(double p_in, double p_out, const double* x, const double* u,
+                                  double* dx) {
+  Compressor comp{CompressorParams(), true};
+  TankParams tank;
+  double flow_total = 0, mo;
+  for (int i = 0; i < 2; ++i) {
+    const double uc[6] = {u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3], p_in, x[10]};
+    comp.derivative(x + 5 * i, uc, dx + 5 * i, &mo);
+    flow_total += mo;
+  }
+  dx[10] = kC2 / tank.volume * (flow_total - valve_flow(x[10], p_out, u[8], tank.D, tank.m_out_c)) * 1e-5;
+}
+
+// GetOutput (systems/parallel_compressors.cc:112-127, serial: both compressors' outputs)
+CMPC_PHD void parallel_output(const double* x, double* y) {
+  Compressor comp{CompressorParams(), true};
+  double y0[2], y1[2];
+  comp.output(x, y0);
+  comp.output(x + 5, y1);
+  y[0] = y0[1];
+  y[1] = y1[1];
+  y[2] = y0[0] - y1[0];
+  y[3] = x[10];
+}
+CMPC_PHD void serial_output(const double* x, double* y) {
+  Compressor comp{CompressorParams(), true};
+  comp.output(x, y);
+  comp.output(x + 5, y + 2);
+}
+
 CMPC_PHD void serial_derivative(double p_in, double p_out, const double* x, const double* u, double* dx) {
   Compressor first{CompressorParams(), true}, follower{CompressorParams(), false};
   double m_out = -1;

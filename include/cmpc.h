@@ -259,6 +259,49 @@ int cmpc_observe_step_host(cmpc_ctx* ctx, const double* u_full, const double* y)
 int cmpc_get_observer_state(cmpc_ctx* ctx, double* host);
 int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
 
+/* Batched plant simulation: the harness's
+ * SimulationSystem for B scenarios on the GPU, one lane per scenario.
+ *   cmpc_sim_reset      SimulationSystem(p_sys, u_offset, x_in) + TimeDelay()
+ *                       (simulation_system.h:50-56, time_delay.h:26-38):
+ *                       x0 (B x ns), u_offset (B x n_inputs), device; dt0 =
+ *                       the integrate_const step (the sampling time)
+ *   cmpc_sim_set_input  SetInput(u) (simulation_system.h:67-70): u_control
+ *                       (B x n_control, device) through the input delay line
+ *                       (time_delay.h:41-58) onto u_offset (GetPlantInput)
+ *   cmpc_sim_integrate  one observation interval [t, t_end] of Integrate
+ *                       (simulation_system.h:108-116): controlled
+ *                       Dormand-Prince with Boost odeint's semantics and the
+ *                       reference's 2-norm error (:121-133); the step size
+ *                       carries over between intervals as in integrate_const
+ *   cmpc_sim_output     GetOutput() (B x n_outputs, device)
+ *   cmpc_sim_plant_input GetPlantInput(u_control) without the delay line (the
+ *                       controller's linearisation input, nerve_center.h:139)
+ * Device arrays: cmpc_sim_state (x), cmpc_sim_input (plant input u_),
+ * cmpc_sim_step_size (dt), cmpc_sim_status (1 = step-size control failed). */
+typedef struct cmpc_sim cmpc_sim;
+int cmpc_sim_create(cmpc_sim** sim, int plant, int B, int device, double p_in, double p_out,
+                    int n_control, const int32_t* delays /* n_control, control order */,
+                    const int32_t* control_index /* ControlInputIndex: plant input of each */);
+int cmpc_sim_destroy(cmpc_sim* sim);
+int cmpc_sim_set_stream(cmpc_sim* sim, void* hip_stream);
+int cmpc_sim_reset(cmpc_sim* sim, const double* x0, const double* u_offset, double dt0);
+int cmpc_sim_set_input(cmpc_sim* sim, const double* u_control);
+int cmpc_sim_plant_input(cmpc_sim* sim, const double* u_control, double* u_full_out);
+int cmpc_sim_integrate(cmpc_sim* sim, double t, double t_end, double eps_abs, double eps_rel);
+int cmpc_sim_output(cmpc_sim* sim, double* y);
+int cmpc_sim_synchronize(cmpc_sim* sim);
+/* Host copies (any pointer may be NULL): x B x ns, plant input B x n_inputs,
+ * step size B, status B. */
+int cmpc_sim_download(cmpc_sim* sim, double* x, double* u_full, double* dt, int32_t* status);
+double* cmpc_sim_state(cmpc_sim* sim);
+double* cmpc_sim_input(cmpc_sim* sim);
+double* cmpc_sim_step_size(cmpc_sim* sim);
+int32_t* cmpc_sim_status(cmpc_sim* sim);
+/* NerveCenter::UpdateUOld (nerve_center.h:313-319): u_control (device,
+ * B x nu_tot, plant control order) += each sub-controller's first move of its
+ * own inputs (du_old after cmpc_iterate; input_order as cmpc_produce_lin). */
+int cmpc_accumulate_moves(cmpc_ctx* ctx, const int32_t* input_order, double* u_control);
+
 /* Device producer: AugmentedLinearizedSystem::Update
  * (libs/aug_lin_sys.cc:145-177, DiscretizeRK4 :232-255) for every scenario b
  * of the context's batch, on the GPU.  Linearises the plant at (x[b],

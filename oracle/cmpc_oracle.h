@@ -19,6 +19,8 @@
  *   or_nerve.c     NerveCenter Jacobi loop / DistributedController::GetInput
  *                  over a batch in the product's lin-record format
  *   or_observer.c  Observer a posteriori / a priori and UpdateU
+ *   or_sim.c       the harness's plant simulation (controlled Dormand-Prince,
+ *                  TimeDelay, GetPlantInput)
  *
  * The product must never route through this library.
  */
@@ -112,6 +114,24 @@ int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
             uint32_t flags, int init, int threads, double* u_old,
             double* du_old, uint32_t* ws, double* du, int32_t* status,
             int32_t* nwsr, uint8_t* trace, int32_t* ntrace);
+
+/* ---- plant simulation (or_plant.c, or_sim.c) ---- */
+/* GetDerivative of the plant (parallel_compressors.cc:9-26, serial_compressors.cc:8-26). */
+int or_plant_derivative(int plant, double p_in, double p_out, const double* x,
+                        const double* u, double* dx);
+/* One observation interval [t, t_end] of SimulationSystem::Integrate
+ * (controlled Dormand-Prince, odeint semantics, see or_sim.c); x in/out,
+ * dt in/out (carried between intervals).  Returns accepted steps, <0 on
+ * failure (500 rejected tries). */
+int or_sim_interval(int plant, double p_in, double p_out, const double* u_full, double* x,
+                    double t, double t_end, double* dt_io, double eps_abs, double eps_rel);
+/* TimeDelay (time_delay.h:26-58): ring = sum(delays) doubles, cur = n_inputs. */
+void or_time_delay_init(int n_inputs, const int32_t* delays, double* ring, int32_t* cur);
+void or_time_delay(int n_inputs, const int32_t* delays, double* ring, int32_t* cur,
+                   const double* u_next, double* u_out);
+/* SimulationSystem::GetPlantInput (simulation_system.h:82-88). */
+void or_plant_input(int n_inputs, int n_control, const int32_t* control_index,
+                    const double* u_offset, const double* u_control, double* u_full);
 
 /* ---- observer (or_observer.c) ---- */
 /* ObserveAPosteriori + x_ += (libs/observer.cc:27-44,

@@ -437,3 +437,31 @@ void or_discretize_rk4(int ns, int nci, double Ts, const double* A,
     fd[i] = s;
   }
 }
+
+/* ParallelCompressors::GetDerivative (systems/parallel_compressors.cc:9-26,
+ * tank: systems/tank.cc:10-24), SerialCompressors::GetDerivative
+ * (systems/serial_compressors.cc:8-26). */
+int or_plant_derivative(int plant, double p_in, double p_out, const double* x,
+                        const double* u, double* dx) {
+  if (plant == OR_PLANT_PARALLEL) {
+    comp_params cp;
+    tank_params tp;
+    comp_default(&cp);
+    tank_default(&tp);
+    double mass_flow_total = 0, m_out;
+    for (int i = 0; i < 2; ++i) {
+      double uc[6];
+      par_comp_input(u, i, x, p_in, uc);
+      comp_derivative(&cp, 1, &m_out, x + 5 * i, uc, dx + 5 * i);
+      mass_flow_total += m_out;
+    }
+    const double m_out_t = valve_mass_flow(x[10], p_out, u[8], tp.D, tp.m_out_c);
+    dx[10] = kSound * kSound / tp.volume * (mass_flow_total - m_out_t) * 1e-5;
+    return 0;
+  }
+  if (plant == OR_PLANT_SERIAL) {
+    ser_derivative(p_in, p_out, x, u, dx);
+    return 0;
+  }
+  return -1;
+}

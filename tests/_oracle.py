@@ -194,3 +194,51 @@ def plant_linearize(plant: int, x, u_full, p_in=1.0, p_out=1.0):
                              dptr(np.ascontiguousarray(u_full, dtype=np.float64)), dptr(A), dptr(B),
                              dptr(C), dptr(f))
     return A.reshape(ns, ns), B.reshape(ns, nci), C.reshape(no, ns), f
+
+
+def _sim_sigs():
+    L = lib()
+    if getattr(L, "_sim_sigs", False):
+        return L
+    P, d, i32 = ctypes.POINTER, ctypes.c_double, ctypes.c_int32
+    L.or_sim_interval.argtypes = [ctypes.c_int, d, d, P(d), P(d), d, d, P(d), d, d]
+    L.or_sim_interval.restype = ctypes.c_int
+    L.or_plant_derivative.argtypes = [ctypes.c_int, d, d, P(d), P(d), P(d)]
+    L.or_time_delay_init.argtypes = [ctypes.c_int, P(i32), P(d), P(i32)]
+    L.or_time_delay.argtypes = [ctypes.c_int, P(i32), P(d), P(i32), P(d), P(d)]
+    L.or_plant_input.argtypes = [ctypes.c_int, ctypes.c_int, P(i32), P(d), P(d), P(d)]
+    L._sim_sigs = True
+    return L
+
+
+class PlantSim:
+    """The harness's SimulationSystem (oracle): TimeDelay -> GetPlantInput ->
+    controlled Dormand-Prince per observation interval (or_sim.c)."""
+
+    def __init__(self, plant, x0, u_offset, delays=(0, 40, 0, 40), control_index=(0, 3, 4, 7),
+                 p_in=1.0, p_out=1.0, dt0=0.05, eps=1e-6):
+        self.L = _sim_sigs()
+        self.plant, self.p_in, self.p_out, self.eps = plant, p_in, p_out, eps
+        self.x = np.array(x0, dtype=np.float64)
+        self.u_offset = np.array(u_offset, dtype=np.float64)
+        self.delays = np.array(delays, dtype=np.int32)
+        self.cidx = np.array(control_index, dtype=np.int32)
+        self.ring = np.zeros(max(1, int(self.delays.sum())))
+        self.cur = np.zeros(len(delays), np.int32)
+        self.L.or_time_delay_init(len(delays), iptr(self.delays), dptr(self.ring), iptr(self.cur))
+        self.u_full = self.u_offset.copy()
+        self.dt = np.array([dt0])
+
+    def set_input(self, u_control):
+        u_next = np.ascontiguousarray(u_control, dtype=np.float64)
+        out = np.zeros(len(self.delays))
+        self.L.or_time_delay(len(self.delays), iptr(self.delays), dptr(self.ring), iptr(self.cur),
+                             dptr(u_next), dptr(out))
+        self.L.or_plant_input(len(self.u_offset), len(self.delays), iptr(self.cidx),
+                              dptr(self.u_offset), dptr(out), dptr(self.u_full))
+
+    def integrate(self, t, t_end):
+        rc = self.L.or_sim_interval(self.plant, self.p_in, self.p_out, dptr(self.u_full),
+                                    dptr(self.x), t, t_end, dptr(self.dt), self.eps, self.eps)
+        assert rc >= 0
+        return rc
