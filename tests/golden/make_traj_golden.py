@@ -38,11 +38,14 @@ def records(path, n):
 
 def main():
     for plant, cfg in CASES:
-        recs = records(os.path.join(REF, plant, "run1", cfg + ".dat"), N_RECORDS)
+        path = os.path.join(REF, plant, "run1", cfg + ".dat")
+        recs = records(path, N_RECORDS)
+        with open(path) as f:  # the first two records verbatim (the writer's format)
+            raw = f.read().split("\n")[:12]
         name = os.path.join(HERE, f"traj_{plant[:3]}_{cfg}.json")
         with open(name, "w") as f:
-            json.dump({"source": f"results/{plant}/run1/{cfg}.dat", "records": recs}, f,
-                      separators=(",", ":"))
+            json.dump({"source": f"results/{plant}/run1/{cfg}.dat", "records": recs,
+                       "raw_first_records": raw}, f, separators=(",", ":"))
         print(name, len(recs))
 
 

@@ -137,3 +137,57 @@ def test_gpu_sim_matches_oracle(plant):
     np.testing.assert_array_equal(uf, np.stack([s.u_full for s in sims]))
     np.testing.assert_allclose(x, ox, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(dt, np.array([s.dt[0] for s in sims]), rtol=1e-10)
+
+
+# ---- the closed-loop driver (cmpc/driver.py) -----------------------------------
+
+def test_dat_writer_matches_reference_format():
+    """The 6-line record text (Eigen's aligned columns, 6 significant digits)
+    equals the reference's own first records, byte for byte, given their values."""
+    import io
+    from cmpc.driver import DatWriter
+    for name in TRAJ:
+        d = json.load(open(os.path.join(HERE, "golden", f"traj_{name}.json")))
+        raw = d["raw_first_records"]
+        buf = io.StringIO()
+        w = DatWriter(buf)
+        for r, ns in zip(d["records"][:2], (int(raw[4]), int(raw[10]))):
+            w.record(r["t"], r["x"], r["u"], r["y"], ns)
+        assert buf.getvalue().split("\n")[:12] == raw, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser"])
+def test_gpu_closed_loop_driver_first_records(name):
+    """Two sampling instants of the device closed loop (plant simulation,
+    observer, QP build, Jacobi iterations, delay line) for a batch of 4
+    identical scenarios: record 0 (u(0), y(0)) and record 1 (x(0.05),
+    y(0.05)) equal the reference's results to 6 digits (both are independent
+    of the missing observer gain: record 1's state depends only on u(0))."""
+    import cmpc
+    import golden_cases as GC
+    from cmpc.driver import ClosedLoop
+    cfg, setup, arr, g = GC.case(name)
+    ctype, plant = name.split("-")
+    traj = load(f"{plant}_{'centralized' if ctype == 'cent' else ctype + '9'}")
+    x0, u0 = cmpc.plant_default(cfg.plant)
+    B = 4
+    from cmpc._abi import CmpcDims
+    L = cmpc.layout_of(CmpcDims.from_config(cfg, 1))
+    M = [np.full((L.nobs, 4), 0.1) for _ in range(cfg.S)]   # arbitrary: no effect on these records
+    loop = ClosedLoop(cfg, arr, M, np.tile(x0, (B, 1)), np.tile(u0, (B, 1)), g["n_iterations"])
+    try:
+        loop.initialize()
+        t, y = loop.step()
+        u = loop.u_ctrl.cpu().numpy()
+        for b in range(B):
+            GC.assert_six_digits(u[b], g["u0"])
+            assert_printed_equal(y.cpu().numpy()[b], traj[0]["y"], "y(0)")
+        x1, _, _, st = loop.sim.download()
+        assert not st.any()
+        t, y1 = loop.step()
+        for b in range(B):
+            assert_printed_equal(x1[b], traj[1]["x"], "x(0.05)")
+            assert_printed_equal(y1.cpu().numpy()[b], traj[1]["y"], "y(0.05)")
+    finally:
+        loop.close()
