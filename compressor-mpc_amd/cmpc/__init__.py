@@ -16,7 +16,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import (CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE, CMPC_QP_INFEASIBLE,
+from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE, CMPC_QP_INFEASIBLE,
                    CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
                    CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
 from .configs import ControllerConfig, SetupFile, reference_config
@@ -24,7 +24,7 @@ from .problem import ControllerArrays, controller_arrays, plant_input_from_plans
 
 __all__ = ["Context", "ControllerConfig", "SetupFile", "reference_config", "controller_arrays",
            "plant_input_from_plans", "plant_lin_record", "plant_default", "plant_output",
-           "layout_of", "qp_solve_batch", "CMPC_APPLY_MOVE", "CMPC_TRACE", "CMPC_QP_OK",
+           "layout_of", "rows_lds_model", "qp_solve_batch", "CMPC_APPLY_MOVE", "CMPC_TRACE", "CMPC_QP_OK",
            "CMPC_QP_MAX_NWSR", "CMPC_QP_INFEASIBLE", "CMPC_QP_NOT_PD"]
 
 
@@ -32,6 +32,16 @@ def layout_of(dims: CmpcDims) -> CmpcLayout:
     L = CmpcLayout()
     check(load_library().cmpc_layout_of(ctypes.byref(dims), ctypes.byref(L)), "cmpc_layout_of")
     return L
+
+
+def rows_lds_model(dims: CmpcDims):
+    """(packed, chosen, lds_bytes): the row build kernel's modelled extra LDS
+    cycles per wave-step for regions packed back to back and for the layout
+    cmpc_build uses (rows_layout.cpp), and its LDS bytes per workgroup."""
+    a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+    check(load_library().cmpc_rows_lds_model(ctypes.byref(dims), ctypes.byref(a), ctypes.byref(b),
+                                              ctypes.byref(n)), "cmpc_rows_lds_model")
+    return a.value, b.value, n.value
 
 
 def plant_default(plant: int):
@@ -236,6 +246,11 @@ class Context:
     # -- hot path --------------------------------------------------------
     def build(self):
         check(self.lib.cmpc_build(self._h), "cmpc_build")
+
+    def set_build_variant(self, variant: int):
+        """CMPC_BUILD_AUTO / CMPC_BUILD_WAVE (one QP per wave) / CMPC_BUILD_ROWS
+        (four QPs per wave, one per DPP row)."""
+        check(self.lib.cmpc_set_build_variant(self._h, int(variant)), "cmpc_set_build_variant")
 
     def init_warmstart(self):
         check(self.lib.cmpc_init_warmstart(self._h), "cmpc_init_warmstart")

@@ -1,0 +1,401 @@
+// Row-layout build kernel: condensation + QP build for FOUR QPs per wave64,
+// one QP per 16-lane DPP row.
+//
+// Same computation as cmpc_build_kernel (cmpc_kernels.hip; reference
+// AdjustAllDelayedStates + GeneratePrediction + GenerateDistributedQP +
+// GenerateQP, include/aug_lin_sys.h:141-154, libs/aug_lin_sys.cc:260-334,
+// include/distributed_solver.h:83-94, libs/mpc_qp_solver.cc:16-40), with the
+// roles moved from rows to registers:
+//
+//   lane j of row R (QP q = 4 g + R), registers
+//     pP[o], o < ny : row o of P_r = L_W' C A^r   (lanes j < ns: column j)
+//     aP[o]         : chain result -> P_{r+1} (lanes j < ns), raw Markov value
+//                     P_r . B_c (Markov lanes ns + c)
+//     pS / aS       : free-response simulation: lanes j < ns state x, lanes
+//                     ns + o the output z_r[o], lanes 16 - nd + k the
+//                     delayed-input values w (carriers)
+//     cv[o], acc[a] : gather lane b < m nu_tot + 1 holds QP column b of output
+//                     row o (move k = b / nu_tot, input c = b % nu_tot; the
+//                     last lane holds z) and accumulates acc[a] = sum_{r,o}
+//                     column_a column_b
+//
+// One horizon step is ny*ns + ns + nd DPP broadcast FMAs (four independent
+// chains interleaved link by link) plus ny*nV gather FMAs, for four QPs at
+// once: 16.25 VALU per QP-step at ny = 3, nV = 4, against 19.75 in the
+// one-QP-per-wave layout, and the sum over outputs stays inside the lane, so
+// no cross-row reduction is needed at the end.
+//
+// Hand-off of Markov / free-response values to the gather lanes through LDS.
+// Every hand-off entry holds the ny outputs side by side ([entry][o]), so the
+// per-output accesses of a step differ by compile-time immediates.
+//   undelayed input : a ring of U + 1 entries [-1, 0 .. U-1]; step u of an
+//                     unrolled group writes entry u, the move-0 lane reads
+//                     entry u and the move-1 lane entry u - 1; after the
+//                     group's last step (and after every single step) the
+//                     value is copied to entry -1, which therefore always
+//                     holds the previous step.
+//   delayed input   : a line of (m - 1) zero entries + (p - D) values written
+//                     at steps r < p - D (then the writer switches to a dump
+//                     area); the gather lanes read a zero area until r = D
+//                     and the line from there on (the delay shifts out of the
+//                     index, as in the one-QP-per-wave kernel).
+//   z               : U entries, written and read in the same step.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "cmpc_internal.h"
+#include "rows_blocks.inc"
+
+// Timing-only ablation switches (tools/ablate_rows.sh); the product build
+// uses CMPC_RX = 0.  1: no LDS hand-off in the loop, 2: every group reads the
+// records of group 0 (cache-resident), 3: no gather accumulation, 4: no
+// hand-off writes (reads kept).
+#ifndef CMPC_RX
+#define CMPC_RX 0
+#endif
+
+template <int NS, int NY, int NUT, int NU, int M, int ND>
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void cmpc_build_rows_kernel(BuildParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int NV = NU * M;
+  constexpr int NG = M * NUT + 1;  // gather lanes: QP columns (move k, input c), then z
+  constexpr int NDW = ND > 0 ? ND : 1;
+  constexpr int U = 4;             // horizon-loop unroll (immediate LDS offsets)
+  static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
+  static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int R = lane >> 4, j = lane & 15;
+  const int pp = P.p, S = P.S, nobs = P.nobs, rec_len = P.rec_len, ndist = P.ndist;
+  const int LQ = P.rows.LQ, WL = P.rows.WL, yls = P.rows.yls;
+  const int nqp = P.nqp;
+  const int ngroups = (nqp + 3) / 4;
+  const int nwaves = gridDim.x * CMPC_BUILD_WAVES;
+
+  double* zeros = smem;
+  double* ylT = smem + P.rows.yl_off;  // [S][NY][yls]  L_W' y_ref, output-major
+  double* lw_all = smem + P.rows.lw_off;
+  double* uw_all = smem + P.rows.uw_off;
+  double* wreg = smem + P.rows.lds_block + wave * P.rows.per_wave;
+  double* lines = wreg;                 // [4][LQ]: per QP, hand-off entries of NY doubles
+  double* chs = wreg + P.rows.ch_off;   // [4][NY][16]  C_hat rows
+  double* wtab = wreg + P.rows.w_off;   // [4][ND][WL]  delay-line inputs w_t
+
+  const int nthr = 64 * CMPC_BUILD_WAVES;
+  for (int e = threadIdx.x; e < S * NY * yls; e += nthr) {
+    const int ss = e / (NY * yls), rem = e - ss * NY * yls;
+    const int o = rem / yls, r = rem - o * yls;
+    // stored negated: the free-response chain starts at kappa + (-yhat_r)
+    ylT[e] = (r < pp) ? -P.cfg[(size_t)ss * P.co.len + P.co.yhat + r * NY + o] : 0.0;
+  }
+  for (int e = threadIdx.x; e < S * NY * NY; e += nthr)
+    lw_all[e] = P.cfg[(size_t)(e / (NY * NY)) * P.co.len + P.co.lwt + e % (NY * NY)];
+  for (int e = threadIdx.x; e < S * NU * NU; e += nthr)
+    uw_all[e] = P.cfg[(size_t)(e / (NU * NU)) * P.co.len + P.co.uwt + e % (NU * NU)];
+  if (threadIdx.x < 16) zeros[threadIdx.x] = 0.0;
+  for (int e = lane; e < P.rows.per_wave; e += 64) wreg[e] = 0.0;  // line heads, dump, slots
+  __syncthreads();
+
+  // ---- per-lane roles (identical for every group) ----
+  const bool st = j < NS;                          // state lane
+  const bool mk = j >= NS && j < NS + NUT;         // Markov writer of input cm
+  const int cm = mk ? j - NS : 0;
+  const bool ol = j >= NS && j < NS + NY;          // free-response output lane
+  const int oo = ol ? j - NS : 0;
+  const bool cl = ND > 0 && j >= 16 - ND;          // delayed-input carrier lane
+  const int kc = cl ? j - (16 - ND) : 0;
+  const bool gl = j < NG;                          // gather lane
+  const bool zlane = j == NG - 1;
+  const int gk = (gl && !zlane) ? j / NUT : 0;
+  const int gc = (gl && !zlane) ? j - gk * NUT : 0;
+  const double smask = (gl && !zlane && gk == M - 1) ? 1.0 : 0.0;  // running-sum column
+  int dg = 0, dm = 0, log_ = 0, lom = 0, dinp[NDW], dlen[NDW], boff[NDW];
+#pragma unroll
+  for (int c = 0; c < NUT; ++c) {
+    if (c == gc) { dg = P.delay[c]; log_ = P.rows.lo[c]; }
+    if (c == cm) { dm = P.delay[c]; lom = P.rows.lo[c]; }
+  }
+#pragma unroll
+  for (int k = 0; k < NDW; ++k) {
+    dinp[k] = (k < ND) ? P.dinput[k] : 0;
+    dlen[k] = (k < ND) ? P.dlen[k] : 0;
+    boff[k] = (k < ND) ? P.boff[k] : 0;
+  }
+  const int nseg = P.rows.nseg;
+  int segb[2 * CMPC_MAX_INPUTS];
+#pragma unroll
+  for (int i = 0; i < 2 * CMPC_MAX_INPUTS; ++i) segb[i] = P.rows.seg[i];
+  double* const qlines = lines + R * LQ;  // this row's QP
+  // readers (entry pointers; output o at +o, step u of a group at +u*NY)
+  const bool rdel = gl && !zlane && dg > 0;
+  const int rsw = (rdel && dg < pp) ? dg : -1;  // step at which a delayed reader starts its line
+  double* const zrow = qlines + P.rows.zr_off;  // never written
+  double* const r_start = !gl ? zrow
+                          : zlane ? qlines + P.rows.z_off
+                          : (dg == 0) ? qlines + log_ + (1 - gk) * NY
+                                      : zrow;
+  double* const r_line = qlines + log_ + (M - 1 - gk) * NY;
+  // writers
+  const bool wdel = mk && dm > 0;
+  double* const dump = qlines + P.rows.dump_off;
+  double* const w_start = !mk ? dump
+                          : (dm == 0) ? qlines + lom + NY
+                          : (pp - dm > 0) ? qlines + lom + (M - 1) * NY
+                                          : dump;
+  const int winc0 = (wdel && pp - dm > 0) ? NY : 0;
+  const int wsw = (wdel && pp - dm > 0) ? pp - dm : -1;
+  const bool tl = M > 1 && mk && dm == 0;  // ring writer: copies each group's last value to entry -1
+  double* const tq = qlines + lom;
+  double* const zq = qlines + P.rows.z_off + oo;
+
+  for (int g = blockIdx.x * CMPC_BUILD_WAVES + wave; g < ngroups; g += nwaves) {
+    const int q = 4 * g + R;
+    const bool qv = q < nqp;
+    const int qq = qv ? q : nqp - 1;
+    const int s = qq % S;
+    const double* rec = P.lin + (size_t)(CMPC_RX == 2 ? R : qq) * rec_len;
+    const double* lwt = lw_all + s * NY * NY;
+    double* chq = chs + R * NY * 16;
+
+    // C_hat = L_W' C_sel (ny x nobs): lane j computes column j of its QP
+    double pP[NY];
+    {
+      double cs[NY];
+#pragma unroll
+      for (int o2 = 0; o2 < NY; ++o2) cs[o2] = (j < nobs) ? rec[P.off_C + o2 * nobs + j] : 0.0;
+#pragma unroll
+      for (int o = 0; o < NY; ++o) {
+        double t = 0.0;
+#pragma unroll
+        for (int o2 = 0; o2 < NY; ++o2)
+          if (o2 >= o) t += lwt[o * NY + o2] * cs[o2];
+        if (j < nobs) chq[o * 16 + j] = t;
+        pP[o] = st ? t : 0.0;  // P_0 = C_hat[:, :ns]
+      }
+    }
+    // P-chain multipliers: A column j (state lanes), B column c (Markov lanes)
+    double mP[NS];
+    if (st) {
+      const double* src = rec + P.off_A + j;
+#pragma unroll
+      for (int l = 0; l < NS; ++l) mP[l] = src[l * NS];
+    } else if (mk) {
+      const double* src = rec + P.off_B + cm;
+#pragma unroll
+      for (int l = 0; l < NS; ++l) mP[l] = src[l * NUT];
+    } else {
+#pragma unroll
+      for (int l = 0; l < NS; ++l) mP[l] = 0.0;
+    }
+    // delay-line inputs w_t of the QP, AdjustAllDelayedStates applied
+    // (include/aug_lin_sys.h:141-154); zero once the line has drained
+    {
+      const double* xa = rec + P.off_x;
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        const double uo = P.u_old[(size_t)qq * NUT + dinp[k]];
+        double* wk = wtab + (R * ND + k) * WL;
+        for (int t = j; t < WL; t += 16) {
+          double v = 0.0;
+          if (t < dlen[k]) v = ((t == 0) ? xa[ndist + k] : xa[boff[k] + t - 1]) - uo;
+          wk[t] = v;
+        }
+      }
+    }
+    // simulation multipliers and chain initialisation
+    double mS[NS + NDW];
+    double base = 0.0, pS = 0.0, yh = 0.0;
+    const double* yp = zeros;
+    int yinc = 0;
+    if (st) {
+      const double* arow = rec + P.off_A + j * NS;
+      const double* brow = rec + P.off_B + j * NUT;
+#pragma unroll
+      for (int l = 0; l < NS; ++l) mS[l] = arow[l];
+#pragma unroll
+      for (int k = 0; k < NDW; ++k) mS[NS + k] = (ND > 0) ? brow[dinp[k]] : 0.0;
+      base = rec[P.off_f + j];
+      pS = base;
+#pragma unroll
+      for (int k = 0; k < ND; ++k) pS += mS[NS + k] * wtab[(R * ND + k) * WL];  // x_1 = f + Adelay w_0
+    } else if (ol) {
+#pragma unroll
+      for (int l = 0; l < NS; ++l) mS[l] = chq[oo * 16 + l];
+#pragma unroll
+      for (int k = 0; k < NDW; ++k) mS[NS + k] = 0.0;
+      // kappa = L_W'(dist + y_prev) = C_hat_dist xa_dist + L_W' y_prev
+      double t = 0.0;
+      for (int d = 0; d < ndist; ++d) t += chq[oo * 16 + NS + d] * rec[P.off_x + d];
+#pragma unroll
+      for (int o2 = 0; o2 < NY; ++o2)
+        if (o2 >= oo) t += lwt[oo * NY + o2] * rec[P.off_y + o2];
+      base = t;
+      const double* yl = ylT + (s * NY + oo) * yls;
+      yh = yl[0];
+      yp = yl + 1;
+      yinc = 1;
+    } else {
+#pragma unroll
+      for (int l = 0; l < NS + NDW; ++l) mS[l] = 0.0;
+      if (cl) {
+        const double* wk = wtab + (R * ND + kc) * WL;
+        pS = wk[1];
+        yh = wk[2];
+        yp = wk + 3;
+        yinc = 1;
+      }
+    }
+    // ring history before t = 0
+    if (tl) {
+#pragma unroll
+      for (int o = 0; o < NY; ++o) tq[o] = 0.0;
+    }
+    double cv[NY], rd[NY], acc[NV];
+#pragma unroll
+    for (int o = 0; o < NY; ++o) cv[o] = rd[o] = 0.0;
+#pragma unroll
+    for (int a = 0; a < NV; ++a) acc[a] = 0.0;
+    double* wq = w_start;
+    double* rq = r_start;
+    int winc = winc0, rinc = 0;
+
+    // L2 prefetch of this wave's next group of records: one dword per
+    // 128-byte line, consumed (and so waited for) only after the horizon
+    // loop, before the output stores; the prologue of the next group then
+    // reads from L2 instead of HBM.
+    float pf0 = 0.f, pf1 = 0.f;
+    if (CMPC_RX != 2) {
+      const int gn = g + nwaves;
+      if (gn < ngroups) {
+        const char* nb = reinterpret_cast<const char*>(P.lin + (size_t)4 * gn * rec_len);
+        const int nbytes = min(4, nqp - 4 * gn) * rec_len * (int)sizeof(double);
+        if (lane * 128 < nbytes) pf0 = *reinterpret_cast<const float*>(nb + lane * 128);
+        if ((lane + 64) * 128 < nbytes) pf1 = *reinterpret_cast<const float*>(nb + (lane + 64) * 128);
+      }
+    }
+
+// one horizon step; u = position inside the unrolled group (immediate LDS
+// offsets).  The LDS reads of a step are consumed one step later (yh at the
+// chain start, rd after the chain), and the scheduling barrier keeps the
+// compiler from sinking them next to their use.
+#define CMPC_ROWS_STEP(u)                                                   \
+  {                                                                         \
+    double aS = base + yh;                                                  \
+    yh = yp[u];                                                             \
+    double aP[NY];                                                          \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o) aP[o] = 0.0;             \
+    rows_chain<NS, NY, ND>(pP, pS, mP, mS, aP, aS);                         \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o)                          \
+        cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
+    if (CMPC_RX != 3) rows_gacc<NY, NUT, NU, M>(cv, acc);                   \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o) pP[o] = aP[o];           \
+    pS = aS;                                                                \
+    if (CMPC_RX != 1 && CMPC_RX != 4) {                                     \
+      if (mk) {                                                             \
+        _Pragma("unroll") for (int o = 0; o < NY; ++o) wq[(u) * NY + o] = aP[o]; \
+      }                                                                     \
+      if (ol) zq[(u) * NY] = aS;                                            \
+    }                                                                       \
+    if (CMPC_RX != 1) {                                                     \
+      _Pragma("unroll") for (int o = 0; o < NY; ++o) rd[o] = rq[(u) * NY + o]; \
+    }                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+  }
+#define CMPC_ROWS_TAIL()                                                    \
+  if (tl) {                                                                 \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o) tq[o] = pP[o];           \
+  }
+
+    int r = 0;
+    for (int sg = 0; sg <= nseg; ++sg) {
+      int r_end = pp;
+#pragma unroll
+      for (int i = 0; i < 2 * CMPC_MAX_INPUTS; ++i)
+        if (i == sg && sg < nseg) r_end = segb[i];
+      for (; r + U <= r_end; r += U) {
+        CMPC_ROWS_STEP(0)
+        CMPC_ROWS_STEP(1)
+        CMPC_ROWS_STEP(2)
+        CMPC_ROWS_STEP(3)
+        CMPC_ROWS_TAIL()
+        wq += U * winc;
+        rq += U * rinc;
+        yp += U * yinc;
+      }
+      for (; r < r_end; ++r) {
+        CMPC_ROWS_STEP(0)
+        CMPC_ROWS_TAIL()
+        wq += winc;
+        rq += rinc;
+        yp += yinc;
+      }
+      if (r == rsw) { rq = r_line; rinc = NY; }
+      if (r == wsw) { wq = dump; winc = 0; }
+    }
+#undef CMPC_ROWS_STEP
+#undef CMPC_ROWS_TAIL
+#pragma unroll
+    for (int o = 0; o < NY; ++o) cv[o] = __builtin_fma(smask, cv[o], rd[o]);
+    rows_gacc<NY, NUT, NU, M>(cv, acc);  // row p - 1
+    asm volatile("" ::"v"(pf0), "v"(pf1));
+
+    if (qv && gl) {
+      double* out = P.qp + (size_t)q * P.qp_len;
+      constexpr int nuo = NUT - NU, nVo = M * nuo;
+      const double* uwt = uw_all + s * NU * NU;
+      const int k2 = j / NUT, c2 = j - k2 * NUT;
+      if (zlane) {
+#pragma unroll
+        for (int a = 0; a < NV; ++a) out[NV * NV + a] = acc[a];  // f
+      } else if (c2 < NU) {
+#pragma unroll
+        for (int a = 0; a < NV; ++a) {  // H = Su' W Su + blkdiag_m(uwt)
+          const double rw = (a / NU == k2) ? uwt[(a % NU) * NU + c2] : 0.0;
+          out[a * NV + k2 * NU + c2] = acc[a] + rw;
+        }
+      } else {
+#pragma unroll
+        for (int a = 0; a < NV; ++a) out[NV * NV + NV + a * nVo + k2 * nuo + (c2 - NU)] = acc[a];  // G
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launcher — explicit instantiation list (cf. the reference's *_list.h)
+// ---------------------------------------------------------------------------
+#define ROWS_CASE(NS_, NY_, NU_, M_)                                                           \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {          \
+    auto kern = cmpc_build_rows_kernel<NS_, NY_, 4, NU_, M_, 2>;                               \
+    const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block +                            \
+                                         (size_t)P.rows.per_wave * CMPC_BUILD_WAVES);          \
+    if (lds > 64 * 1024)                                                                       \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);         \
+    int per_cu = 0;                                                                            \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * CMPC_BUILD_WAVES,     \
+                                                     lds) != hipSuccess || per_cu < 1)         \
+      per_cu = std::max<int>(1, (int)((160 * 1024) / lds));                                    \
+    const int need = std::max(1, ((P.nqp + 3) / 4 + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES); \
+    const int grid = std::max(1, std::min(need, P.cus * per_cu));                              \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * CMPC_BUILD_WAVES), lds, s, P);              \
+    return 0;                                                                                  \
+  }
+
+int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!P.rows.ok) return -1;
+  ROWS_CASE(11, 3, 2, 2)  // parallel coop        (ControlledOutputIndices <0,1,3>)
+  ROWS_CASE(11, 2, 2, 2)  // parallel ncoop
+  ROWS_CASE(11, 3, 4, 2)  // parallel centralized
+  ROWS_CASE(10, 2, 2, 2)  // serial ncoop
+  ROWS_CASE(10, 4, 2, 2)  // serial coop          (all four outputs)
+  ROWS_CASE(10, 4, 4, 2)  // serial centralized
+  ROWS_CASE(11, 3, 2, 1)
+  return -1;
+}

@@ -97,6 +97,8 @@ struct cmpc_ctx {
   size_t stage_cap = 0;
   int obs_io[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS] = {};
   int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
+  // build kernel selection (cmpc_set_build_variant)
+  int build_variant = CMPC_BUILD_AUTO;
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
@@ -1053,6 +1055,14 @@ static void build_lds_layout(const cmpc_dims& d, const cmpc_layout& L, BuildPara
   std::sort(P->bound, P->bound + P->nbound);
 }
 
+int cmpc_set_build_variant(cmpc_ctx* c, int variant) {
+  if (!c) return fail("null context");
+  if (variant != CMPC_BUILD_AUTO && variant != CMPC_BUILD_WAVE && variant != CMPC_BUILD_ROWS)
+    return fail("cmpc_set_build_variant: unknown variant");
+  c->build_variant = variant;
+  return 0;
+}
+
 int cmpc_build(cmpc_ctx* c) {
   if (!c) return fail("null context");
   if (ensure_cfg(c)) return -1;
@@ -1105,9 +1115,20 @@ int cmpc_build(cmpc_ctx* c) {
     P.cus = cus;
     P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
   }
+  cmpc_rows_layout(d, L.nd, L.nobs, &P.rows);  // cached per dimension set
   hipEvent_t e0 = nullptr;
   if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
-  if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
+  int rc = -1;
+  // AUTO: the row kernel while its LDS allows two or more workgroups per CU
+  // (at one workgroup, i.e. one wave per SIMD, the one-QP-per-wave kernel is
+  // faster: coop p = 100 measured 0.94 vs 0.86 ms)
+  const size_t rows_lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * CMPC_BUILD_WAVES);
+  const bool rows_auto = rows_lds <= 80 * 1024;
+  if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_auto))
+    rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
+  if (rc && c->build_variant == CMPC_BUILD_ROWS)
+    return fail("row-layout build kernel not available for these dimensions");
+  if (rc && cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
     return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
   if (check_launch("build kernel")) return -1;
   return timed_end(c, CMPC_KERNEL_BUILD, e0);

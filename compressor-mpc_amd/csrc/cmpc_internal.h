@@ -19,6 +19,22 @@ struct CfgOffsets {
   int lwt, yhat, uwt, lower, upper, rlower, rupper, len;
 };
 
+// LDS layout of the row-layout build kernel (build_rows.hip), doubles.
+// Block region: [zeros 16][yhat S x NY x yls (output-major)][lwt][uwt].
+// Wave region : [hand-off 4 x LQ][C_hat 4 x NY x 16][w 4 x ND x WL].
+// Hand-off area of one QP, in entries of NY doubles ([entry][output]): per
+// input c at lo[c] a ring of U + 1 entries (undelayed) or m - 1 zero entries
+// + max(0, p - D_c) values (delayed); then a dump area, the free-response z
+// entries and a zero area (U entries each).
+struct RowsLayout {
+  int ok;                        // the row kernel can run these dimensions
+  int lds_block, per_wave;
+  int yl_off, yls, lw_off, uw_off;
+  int LQ, lo[CMPC_MAX_INPUTS], dump_off, z_off, zr_off;
+  int ch_off, w_off, WL;
+  int nseg, seg[2 * CMPC_MAX_INPUTS];  // ascending distinct D and p - D inside (0, p)
+};
+
 struct BuildParams {
   const double* lin;     // nqp * rec_len
   const double* cfg;     // S * cfg.len
@@ -47,6 +63,7 @@ struct BuildParams {
   int bound[CMPC_MAX_INPUTS];
   int grid;                      // workgroups needed (one QP per wave); launcher caps it
   int cus;                       // compute units of the device
+  RowsLayout rows;               // row-layout kernel (four QPs per wave)
 };
 
 struct SolveParams {
@@ -139,6 +156,14 @@ struct CoupledParams {
 // Kernel launchers (cmpc_kernels.hip, produce.hip, coupled.hip).  Return 0 or -1 (unsupported dims).
 int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
                       void* stream);
+// Row-layout build kernel (build_rows.hip); -1 when not instantiated / not usable.
+int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
+                           void* stream);
+// LDS layout of the row kernel, chosen by a bank-conflict model of its
+// horizon loop (rows_layout.cpp); cached per dimension set, thread-safe.
+void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out);
+// modelled extra LDS cycles per wave-step of the horizon loop for one wave
+double cmpc_rows_layout_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave);
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);

@@ -1,0 +1,315 @@
+// LDS layout of the row-layout build kernel (build_rows.hip), chosen by a
+// bank-conflict model of its horizon loop.
+//
+// The kernel's LDS offsets are all runtime parameters (RowsLayout), so the
+// host can place every region freely.  The horizon loop issues, per step and
+// wave (tools/lds_rows_sim.py is the same model in Python):
+//   ds_read_b64   yh   = yp[u]                 (zeros / L_W'y_ref / carriers)
+//   ds_write_b64  wq[u*NY + o], o < NY          (Markov writers, 4 lanes a row)
+//   ds_write_b64  zq[u*NY]                      (free-response writers)
+//   ds_read2_b64 + ds_read_b64  rq[u*NY + o]    (gather lanes)
+//   per unrolled group: ds_write_b64 tq[o]      (ring history)
+// and MI355X_MICROARCH.md §LDS gives their banking: ds_read_b64 in two
+// 32-lane groups on 32 double-wide banks, ds_read2_b64 / ds_write_b64 in four
+// 16-lane groups on 16; every extra distinct address on a bank costs one LDS
+// cycle.  Packed naively (regions back to back) the loop takes ≈ 28 extra
+// LDS cycles per wave-step at coop p = 50, which PMC confirmed
+// (SQ_LDS_BANK_CONFLICT ≈ 30 per wave-step).  A deterministic search over the
+// order of the per-input lines and a few doubles of padding between regions,
+// within the LDS budget that keeps the same number of workgroups per CU,
+// brings the model to ≈ 2.
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "cmpc_internal.h"
+
+namespace {
+
+constexpr int kU = 4;             // horizon unroll of the kernel (U in build_rows.hip)
+constexpr int kLdsBytes = 160 * 1024;
+
+struct Pads {
+  int order[CMPC_MAX_INPUTS];
+  int pad_c[CMPC_MAX_INPUTS];
+  int dump, z, zr, LQ, yl, yls, w, WL;
+};
+
+int up(int v, int a) { return (v + a - 1) / a * a; }
+
+// The layout for given paddings (all offsets in doubles).  Returns the LDS
+// bytes per workgroup.
+size_t make_layout(const cmpc_dims& d, int nd, const Pads& pd, RowsLayout* R) {
+  std::memset(R, 0, sizeof *R);
+  const int M = d.m, ny = d.ny, U = kU;
+  int o = 0;
+  for (int i = 0; i < d.nu_tot; ++i) {
+    const int c = pd.order[i];
+    o += pd.pad_c[c];
+    R->lo[c] = o;
+    o += ny * ((d.delay[c] == 0) ? U + 1 : (M - 1) + std::max(0, d.p - d.delay[c]));
+  }
+  o += pd.dump;
+  R->dump_off = o;
+  o += U * ny;
+  o += pd.z;
+  R->z_off = o;
+  o += U * ny;
+  o += pd.zr;
+  R->zr_off = o;
+  o += U * ny;
+  R->LQ = up(o, 2) + 2 * pd.LQ;
+  R->ch_off = 4 * R->LQ;
+  R->w_off = R->ch_off + 4 * ny * 16 + pd.w;
+  R->WL = up(d.p + 2 + U, 2) + pd.WL;
+  R->per_wave = up(R->w_off + 4 * nd * R->WL, 2);
+  R->yls = d.p + U + pd.yls;
+  R->yl_off = 16 + pd.yl;
+  R->lw_off = R->yl_off + d.S * ny * R->yls;
+  R->uw_off = R->lw_off + d.S * ny * ny;
+  R->lds_block = up(R->uw_off + d.S * d.nu * d.nu, 2);
+  // loop segments: distinct D (delayed readers start) and p - D (delayed
+  // writers stop) inside (0, p), ascending
+  R->nseg = 0;
+  auto add = [&](int v) {
+    if (v <= 0 || v >= d.p) return;
+    for (int i = 0; i < R->nseg; ++i)
+      if (R->seg[i] == v) return;
+    R->seg[R->nseg++] = v;
+  };
+  for (int c = 0; c < d.nu_tot; ++c)
+    if (d.delay[c] > 0) {
+      add(d.delay[c]);
+      add(d.p - d.delay[c]);
+    }
+  std::sort(R->seg, R->seg + R->nseg);
+  return sizeof(double) * ((size_t)R->lds_block + (size_t)R->per_wave * CMPC_BUILD_WAVES);
+}
+
+// max over banks of the distinct addresses on a bank, for lanes [g0, g0+n)
+int group_cycles(const int* a, const bool* act, int g0, int n, int nbank) {
+  int seen[64], ns = 0, cnt[64] = {0}, mx = 1;
+  for (int i = g0; i < g0 + n; ++i) {
+    if (!act[i]) continue;
+    bool dup = false;
+    for (int k = 0; k < ns && !dup; ++k) dup = seen[k] == a[i];
+    if (dup) continue;
+    seen[ns++] = a[i];
+    const int b = ((a[i] % nbank) + nbank) % nbank;
+    mx = std::max(mx, ++cnt[b]);
+  }
+  return mx;
+}
+
+// Extra LDS cycles per wave-step of the horizon loop for wave `wave`; the
+// per-lane pointer arithmetic is the kernel's (build_rows.hip).
+double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave) {
+  const int NS = d.ns, NY = d.ny, NUT = d.nu_tot, M = d.m, ND = nd, S = d.S, p = d.p, U = kU;
+  const int NG = M * NUT + 1;
+  const int wreg = R.lds_block + wave * R.per_wave;
+  int rq[64], rinc[64], rline[64], rsw[64], wq[64], winc[64], wsw[64], dump[64], yp[64], yinc[64];
+  int zq[64], tq[64];
+  bool mk[64], ol[64], tl[64], all[64];
+  for (int lane = 0; lane < 64; ++lane) {
+    const int Rw = lane >> 4, j = lane & 15, s = Rw % S;
+    const int ql = wreg + Rw * R.LQ;
+    const bool st = j < NS;
+    mk[lane] = j >= NS && j < NS + NUT;
+    const int cm = mk[lane] ? j - NS : 0;
+    ol[lane] = j >= NS && j < NS + NY;
+    const int oo = ol[lane] ? j - NS : 0;
+    const bool cl = ND > 0 && j >= 16 - ND;
+    const int kc = cl ? j - (16 - ND) : 0;
+    const bool gl = j < NG, zl = j == NG - 1;
+    const int gk = (gl && !zl) ? j / NUT : 0;
+    const int gc = (gl && !zl) ? j - gk * NUT : 0;
+    const int dg = d.delay[gc], dm = d.delay[cm];
+    const int zrow = ql + R.zr_off;
+    rq[lane] = !gl ? zrow : zl ? ql + R.z_off : (dg == 0) ? ql + R.lo[gc] + (1 - gk) * NY : zrow;
+    rinc[lane] = 0;
+    rline[lane] = ql + R.lo[gc] + (M - 1 - gk) * NY;
+    const bool rdel = gl && !zl && dg > 0;
+    rsw[lane] = (rdel && dg < p) ? dg : -1;
+    const bool wdel = mk[lane] && dm > 0;
+    dump[lane] = ql + R.dump_off;
+    wq[lane] = !mk[lane] ? dump[lane]
+               : (dm == 0) ? ql + R.lo[cm] + NY
+               : (p - dm > 0) ? ql + R.lo[cm] + (M - 1) * NY
+                              : dump[lane];
+    winc[lane] = (wdel && p - dm > 0) ? NY : 0;
+    wsw[lane] = (wdel && p - dm > 0) ? p - dm : -1;
+    tl[lane] = M > 1 && mk[lane] && dm == 0;
+    tq[lane] = ql + R.lo[cm];
+    zq[lane] = ql + R.z_off + oo;
+    if (st) {
+      yp[lane] = 0; yinc[lane] = 0;
+    } else if (ol[lane]) {
+      yp[lane] = R.yl_off + (s * NY + oo) * R.yls + 1; yinc[lane] = 1;
+    } else if (cl) {
+      yp[lane] = wreg + R.w_off + (Rw * ND + kc) * R.WL + 3; yinc[lane] = 1;
+    } else {
+      yp[lane] = 0; yinc[lane] = 0;
+    }
+    all[lane] = true;
+  }
+  long extra = 0, steps = 0;
+  int a[64], b[64];
+  auto read_b64 = [&](const int* x) {
+    extra += group_cycles(x, all, 0, 32, 32) - 1 + group_cycles(x, all, 32, 32, 32) - 1;
+  };
+  auto by16 = [&](const int* x, const bool* act) {
+    for (int g = 0; g < 64; g += 16) extra += group_cycles(x, act, g, 16, 16) - 1;
+  };
+  auto step = [&](int u) {
+    ++steps;
+    for (int l = 0; l < 64; ++l) a[l] = yp[l] + u;
+    read_b64(a);
+    for (int o = 0; o < NY; ++o) {
+      for (int l = 0; l < 64; ++l) a[l] = wq[l] + u * NY + o;
+      by16(a, mk);
+    }
+    for (int l = 0; l < 64; ++l) a[l] = zq[l] + u * NY;
+    by16(a, ol);
+    for (int o = 0; o < NY;) {
+      for (int l = 0; l < 64; ++l) a[l] = rq[l] + u * NY + o;
+      if (o + 1 < NY) {  // the compiler pairs the reads into ds_read2_b64
+        for (int l = 0; l < 64; ++l) b[l] = a[l] + 1;
+        by16(a, all);
+        by16(b, all);
+        o += 2;
+      } else {
+        read_b64(a);
+        o += 1;
+      }
+    }
+  };
+  auto tail = [&]() {
+    for (int o = 0; o < NY; ++o) {
+      for (int l = 0; l < 64; ++l) a[l] = tq[l] + o;
+      by16(a, tl);
+    }
+  };
+  auto advance = [&](int k) {
+    for (int l = 0; l < 64; ++l) {
+      wq[l] += k * winc[l];
+      rq[l] += k * rinc[l];
+      yp[l] += k * yinc[l];
+    }
+  };
+  int r = 0;
+  for (int sg = 0; sg <= R.nseg; ++sg) {
+    const int r_end = sg < R.nseg ? R.seg[sg] : p;
+    for (; r + U <= r_end; r += U) {
+      for (int u = 0; u < U; ++u) step(u);
+      tail();
+      advance(U);
+    }
+    for (; r < r_end; ++r) {
+      step(0);
+      tail();
+      advance(1);
+    }
+    for (int l = 0; l < 64; ++l) {
+      if (r == rsw[l]) { rq[l] = rline[l]; rinc[l] = NY; }
+      if (r == wsw[l]) { wq[l] = dump[l]; winc[l] = 0; }
+    }
+  }
+  return steps ? (double)extra / steps : 0.0;
+}
+
+uint64_t lcg(uint64_t& s) {
+  s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+  return s >> 33;
+}
+
+
+}  // namespace
+
+void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out) {
+  std::memset(out, 0, sizeof *out);
+  if (d.m < 1 || d.m > 2 || nobs > 16) return;
+  static std::mutex mu;
+  static std::map<std::vector<int>, RowsLayout> cache;
+  std::vector<int> key{d.ns, d.ny, d.nu, d.nu_tot, d.m, d.p, d.S, nd, nobs};
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) key.push_back(d.delay[c]);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      *out = it->second;
+      return;
+    }
+  }
+  Pads base{};
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
+  RowsLayout best;
+  const size_t base_bytes = make_layout(d, nd, base, &best);
+  // CMPC_ROWS_LAYOUT=packed: regions back to back (diagnostic A/B timing)
+  const char* env = std::getenv("CMPC_ROWS_LAYOUT");
+  const bool packed = env && std::strcmp(env, "packed") == 0;
+  if (packed) {
+    best.ok = base_bytes <= (size_t)kLdsBytes;
+  } else if (base_bytes <= (size_t)kLdsBytes) {
+    // keep the workgroups per CU of the packed layout
+    const int wg = (int)(kLdsBytes / base_bytes);
+    const size_t budget = (size_t)(kLdsBytes / wg) / 512 * 512;
+    double best_cost = loop_conflicts(d, nd, best, 0);
+    Pads bp = base;
+    uint64_t seed = 0x5eedULL;
+    for (int it = 0; it < 400 && best_cost > 0.0; ++it) {
+      Pads cand = bp;
+      const int nchg = 1 + (int)(lcg(seed) % 3);
+      for (int k = 0; k < nchg; ++k) {
+        const int which = (int)(lcg(seed) % (d.nu_tot + 8));
+        const int v = (int)(lcg(seed) % 16);
+        if (which < d.nu_tot) cand.pad_c[which] = v;
+        else {
+          int* f[8] = {&cand.dump, &cand.z, &cand.zr, &cand.LQ, &cand.yl, &cand.yls, &cand.w, &cand.WL};
+          *f[which - d.nu_tot] = (which - d.nu_tot == 3) ? v % 4 : v;
+        }
+      }
+      if (lcg(seed) % 10 < 3) {
+        for (int i = d.nu_tot - 1; i > 0; --i) std::swap(cand.order[i], cand.order[lcg(seed) % (i + 1)]);
+      }
+      RowsLayout R;
+      if (make_layout(d, nd, cand, &R) > budget) continue;
+      const double cost = loop_conflicts(d, nd, R, 0);
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = R;
+        bp = cand;
+      }
+    }
+    best.ok = make_layout(d, nd, bp, &best) <= (size_t)kLdsBytes;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = best;
+  *out = best;
+}
+
+double cmpc_rows_layout_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave) {
+  return loop_conflicts(d, nd, R, wave);
+}
+
+extern "C" int cmpc_rows_lds_model(const cmpc_dims* d, double* packed_cycles, double* chosen_cycles,
+                                   int32_t* lds_bytes) {
+  if (!d) return -1;
+  cmpc_layout L;
+  if (cmpc_layout_of(d, &L)) return -1;
+  RowsLayout R;
+  cmpc_rows_layout(*d, L.nd, L.nobs, &R);
+  if (!R.ok) return -1;
+  Pads base{};
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
+  RowsLayout P0;
+  make_layout(*d, L.nd, base, &P0);
+  if (packed_cycles) *packed_cycles = loop_conflicts(*d, L.nd, P0, 0);
+  if (chosen_cycles) *chosen_cycles = loop_conflicts(*d, L.nd, R, 0);
+  if (lds_bytes)
+    *lds_bytes = (int32_t)(sizeof(double) * ((size_t)R.lds_block + (size_t)R.per_wave * CMPC_BUILD_WAVES));
+  return 0;
+}

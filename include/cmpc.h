@@ -144,6 +144,22 @@ int cmpc_bind_lin(cmpc_ctx* ctx, const double* lin_device);
 
 /* Hot path. */
 int cmpc_build(cmpc_ctx* ctx);
+/* Build-kernel selection for cmpc_build (same H, f, G within rounding):
+ * CMPC_BUILD_ROWS four QPs per wave, one per 16-lane DPP row (m <= 2, LDS
+ * fits); CMPC_BUILD_WAVE one QP per wave (every instantiated dimension set);
+ * CMPC_BUILD_AUTO (default) rows where its LDS leaves >= 2 workgroups per CU,
+ * else wave. */
+#define CMPC_BUILD_AUTO 0
+#define CMPC_BUILD_WAVE 1
+#define CMPC_BUILD_ROWS 2
+int cmpc_set_build_variant(cmpc_ctx* ctx, int variant);
+/* Diagnostic (no GPU needed): the row kernel's LDS layout for *dims as
+ * cmpc_build chooses it.  Writes the bank-conflict model's extra LDS cycles
+ * per wave-step of the horizon loop (wave 0) for the packed layout (regions
+ * back to back) and for the chosen one, and the chosen layout's LDS bytes per
+ * workgroup.  Returns 0, or -1 if the row kernel cannot run these dims. */
+int cmpc_rows_lds_model(const cmpc_dims* dims, double* packed_cycles, double* chosen_cycles,
+                        int32_t* lds_bytes);
 int cmpc_init_warmstart(cmpc_ctx* ctx);
 int cmpc_iterate(cmpc_ctx* ctx, int K, uint32_t flags);
 int cmpc_step(cmpc_ctx* ctx, int K, uint32_t flags);

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     text = open(os.path.join(ROOT, "include", "cmpc.h")).read()
-    return set(re.findall(r"^\s*(?:int|void\*|const char\*)\s+(cmpc_\w+)\(", text, re.M))
+    return set(re.findall(r"^\s*(?:int|void\*|const char\*|double\*|int32_t\*)\s+(cmpc_\w+)\(", text, re.M))
 
 
 def test_header_and_binding_agree():
@@ -82,3 +82,20 @@ def test_library_fails_loudly_without_device():
     cfg = reference_config("par", "coop", p=20)
     with pytest.raises(RuntimeError):
         cmpc.Context(cfg, 4)
+
+
+@pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "ncoop", 50), ("par", "cent", 50),
+                                           ("ser", "coop", 50), ("par", "coop", 20)])
+def test_rows_lds_layout_search(plant, ctype, p):
+    """The row build kernel's LDS layout (rows_layout.cpp): the bank-conflict
+    model of its horizon loop is no worse than regions packed back to back
+    (at the bench config, coop p = 50: 28 -> <= 3 extra LDS cycles per
+    wave-step), within the LDS budget that keeps the packed layout's
+    workgroups per CU."""
+    cfg = reference_config(plant, ctype, p=p)
+    packed, chosen, nbytes = cmpc.rows_lds_model(CmpcDims.from_config(cfg, 8))
+    assert chosen <= packed
+    assert 0 < nbytes <= 160 * 1024
+    if (plant, ctype, p) == ("par", "coop", 50):
+        assert packed > 20 and chosen <= 3.0
+        assert 160 * 1024 // nbytes == 4  # still four workgroups (16 waves) per CU

@@ -75,14 +75,19 @@ def setup_for(plant, ctype):
     return GC.case(name)
 
 
+@pytest.mark.parametrize("variant", [cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_ROWS])
 @pytest.mark.parametrize("plant,ctype,p", BUILD_CASES)
-def test_gpu_build_matches_oracle(plant, ctype, p):
+def test_gpu_build_matches_oracle(plant, ctype, p, variant):
+    """Both build kernels (one QP per wave / four QPs per wave, one per DPP
+    row) against the oracle; B*S = 94 QPs, not a multiple of four, so the
+    row kernel's last group is partial."""
     _, setup, _, _ = setup_for(plant, ctype)
     cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
-    B = 48
+    B = 47
     lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=11 + p)
     with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.set_build_variant(variant)
         ctx.build()
         H, f, G = ctx.download_qp()
     Ho, fo, Go = oracle_qps(cfg, arr, lin, u_old)
@@ -95,6 +100,31 @@ def test_gpu_build_matches_oracle(plant, ctype, p):
         if cfg.nVo:
             sG = max(np.abs(Go[q]).max(), 1e-300)
             np.testing.assert_allclose(G[q], Go[q], rtol=0, atol=1e-11 * max(sG, 1e-6 * sH))
+
+
+@pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "cent", 50),
+                                           ("ser", "coop", 100), ("par", "coop", 20)])
+def test_gpu_build_variants_agree_large(plant, ctype, p):
+    """Row-layout vs one-QP-per-wave build on a large batch (persistent grid,
+    several groups per wave): H, f, G agree to FP64 reassociation."""
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 20001
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=101 + p, n_distinct=512)
+    out = {}
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        for v in (cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_ROWS):
+            ctx.set_build_variant(v)
+            ctx.build()
+            out[v] = ctx.download_qp()
+    (Hw, fw, Gw), (Hr, fr, Gr) = out[cmpc.CMPC_BUILD_WAVE], out[cmpc.CMPC_BUILD_ROWS]
+    assert np.isfinite(Hr).all() and np.isfinite(fr).all() and np.isfinite(Gr).all()
+    sH = np.abs(Hw).max(axis=(1, 2))
+    assert (np.abs(Hr - Hw).max(axis=(1, 2)) <= 1e-11 * sH).all()
+    assert (np.abs(fr - fw).max(axis=1) <= 1e-10 * np.maximum(np.abs(fw).max(axis=1), 1e-6 * sH)).all()
+    if cfg.nVo:
+        assert (np.abs(Gr - Gw).max(axis=(1, 2)) <= 1e-11 * np.maximum(np.abs(Gw).max(axis=(1, 2)), 1e-6 * sH)).all()
 
 
 def test_gpu_solver_bitexact_on_identical_inputs():

@@ -1,5 +1,6 @@
 """Time cmpc_build alone at several horizons (per-step vs fixed per-QP cost).
-CMPC_TB_CASE=plant-ctype selects the configuration (default par-coop)."""
+CMPC_TB_CASE=plant-ctype selects the configuration (default par-coop);
+CMPC_TB_VARIANT=wave|rows|both selects the build kernel (default both)."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
@@ -10,15 +11,21 @@ from cmpc.synthetic import synthetic_batch
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 PS = [int(a) for a in sys.argv[2:]] or [2, 10, 25, 50, 100]
 PLANT, CTYPE = os.environ.get("CMPC_TB_CASE", "par-coop").split("-")
+VAR = {"wave": [cmpc.CMPC_BUILD_WAVE], "rows": [cmpc.CMPC_BUILD_ROWS],
+       "both": [cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_ROWS]}[os.environ.get("CMPC_TB_VARIANT", "both")]
 for p in PS:
     cfg = cmpc.reference_config(PLANT, CTYPE, p=p)
     arr = cmpc.controller_arrays(cfg, reference_setup(PLANT, CTYPE))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
-    with cmpc.Context(cfg, B) as ctx:
-        ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
-        for _ in range(3): ctx.build()
-        ctx.synchronize()
-        ctx.enable_timing(True)
-        for _ in range(10): ctx.build()
-        ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
-        print(f"p={p:4d}  build {ms/n:.4f} ms  per QP-step {ms/n*1e6/(B*cfg.S*p):.3f} ns  ({PLANT}-{CTYPE})", flush=True)
+    for v in VAR:
+        with cmpc.Context(cfg, B) as ctx:
+            ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
+            ctx.set_build_variant(v)
+            for _ in range(3): ctx.build()
+            ctx.synchronize()
+            ctx.enable_timing(True)
+            for _ in range(10): ctx.build()
+            ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+            name = "wave" if v == cmpc.CMPC_BUILD_WAVE else "rows"
+            print(f"p={p:4d}  {name} build {ms/n:.4f} ms  per QP-step {ms/n*1e6/(B*cfg.S*p):.3f} ns"
+                  f"  ({PLANT}-{CTYPE})", flush=True)
