@@ -273,11 +273,13 @@ def main():
     f_build = build_flops(cfg, L.naug, L.nd)
     achieved_tf = B * S * f_build / avg_build_s / 1e12
     traffic = None
+    build_kernel = ("cmpc_build_rows_kernel" if ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS
+                    else "cmpc_build_kernel")
     pmc = os.path.join(ROOT, "profiles", "pmc_build_coop_p50.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
-            if rec.get("batch") == B:
+            if rec.get("batch") == B and rec.get("kernel") == build_kernel:
                 traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -307,7 +309,7 @@ def main():
         "roofline": {
             "bound": "mfma",
             "pipe": "fp64 VALU (v_fmac_f64_dpp); MI355X FP64 vector peak = FP64 matrix peak",
-            "kernel": "cmpc_build_kernel<NS=11,NY=3,NUT=4,NU=2,M=2,ND=2>",
+            "kernel": build_kernel + "<NS=11,NY=3,NUT=4,NU=2,M=2,ND=2>",
             "achieved": achieved_tf,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",

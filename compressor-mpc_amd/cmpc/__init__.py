@@ -252,6 +252,12 @@ class Context:
         (four QPs per wave, one per DPP row)."""
         check(self.lib.cmpc_set_build_variant(self._h, int(variant)), "cmpc_set_build_variant")
 
+    def last_build_kernel(self) -> int:
+        """CMPC_BUILD_WAVE / CMPC_BUILD_ROWS: the kernel the last build() ran."""
+        v = self.lib.cmpc_last_build_kernel(self._h)
+        check(min(v, 0), "cmpc_last_build_kernel")
+        return v
+
     def init_warmstart(self):
         check(self.lib.cmpc_init_warmstart(self._h), "cmpc_init_warmstart")
 

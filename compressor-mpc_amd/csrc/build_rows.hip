@@ -49,15 +49,14 @@
 #include "rows_blocks.inc"
 
 // Timing-only ablation switches (tools/ablate_rows.sh); the product build
-// uses CMPC_RX = 0.  1: no LDS hand-off in the loop, 2: every group reads the
-// records of group 0 (cache-resident), 3: no gather accumulation, 4: no
-// hand-off writes (reads kept).
+// uses CMPC_RX = 0.  1: no LDS hand-off in the loop, 3: no gather
+// accumulation, 4: no hand-off writes (reads kept).
 #ifndef CMPC_RX
 #define CMPC_RX 0
 #endif
 
 template <int NS, int NY, int NUT, int NU, int M, int ND>
-__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(4, 4)))
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -156,97 +155,144 @@ void cmpc_build_rows_kernel(BuildParams P) {
     const bool qv = q < nqp;
     const int qq = qv ? q : nqp - 1;
     const int s = qq % S;
-    const double* rec = P.lin + (size_t)(CMPC_RX == 2 ? R : qq) * rec_len;
     const double* lwt = lw_all + s * NY * NY;
     double* chq = chs + R * NY * 16;
 
-    // C_hat = L_W' C_sel (ny x nobs): lane j computes column j of its QP
-    double pP[NY];
+    // ---- the group's four records -> LDS in one round trip ----
+    // Consecutive QPs' records are contiguous, so the group's 4 rec_len
+    // doubles are one coalesced block, copied with 16-byte LDS-DMA loads
+    // (global_load_lds_dwordx4: no VGPRs) into the wave's region, which the
+    // tables below overwrite once the records are read.  (Reading the records
+    // with per-lane global loads took ~15 dependent round trips per group, and
+    // L2 evicted records in between: 2.5x the algorithmic HBM bytes.)
     {
-      double cs[NY];
-#pragma unroll
-      for (int o2 = 0; o2 < NY; ++o2) cs[o2] = (j < nobs) ? rec[P.off_C + o2 * nobs + j] : 0.0;
-#pragma unroll
-      for (int o = 0; o < NY; ++o) {
-        double t = 0.0;
-#pragma unroll
-        for (int o2 = 0; o2 < NY; ++o2)
-          if (o2 >= o) t += lwt[o * NY + o2] * cs[o2];
-        if (j < nobs) chq[o * 16 + j] = t;
-        pP[o] = st ? t : 0.0;  // P_0 = C_hat[:, :ns]
+      const int nq = min(4, nqp - 4 * g);
+      const int nchunk = nq * rec_len / 2;
+      const double* gsrc = P.lin + (size_t)4 * g * rec_len;
+      for (int c0 = 0; c0 < nchunk; c0 += 64) {
+        if (c0 + lane < nchunk)
+          __builtin_amdgcn_global_load_lds(
+              (__attribute__((address_space(1))) void*)(gsrc + 2 * (c0 + lane)),
+              (__attribute__((address_space(3))) void*)(wreg + 2 * c0), 16, 0, 0);
       }
     }
+    double uo[NDW];
+#pragma unroll
+    for (int k = 0; k < NDW; ++k) uo[k] = (k < ND) ? P.u_old[(size_t)qq * NUT + dinp[k]] : 0.0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double* srec = wreg + R * rec_len;  // this row's record (staged)
+    const double* xa = srec + P.off_x;
+    double xw[NDW][4];  // delay-line sources of w_t, t = j + 16 i < 64
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = j + 16 * i;
+        xw[k][i] = (t < dlen[k]) ? ((t == 0) ? xa[ndist + k] : xa[boff[k] + t - 1]) : 0.0;
+      }
+    }
+    double cs[NY];  // controlled rows of C, column j
+#pragma unroll
+    for (int o2 = 0; o2 < NY; ++o2) cs[o2] = (j < nobs) ? srec[P.off_C + o2 * nobs + j] : 0.0;
+    constexpr int KX = 16 - NS;  // >= disturbance states (nobs = ns + ndist <= 16)
+    double kx[KX], ky[NY];
+#pragma unroll
+    for (int d = 0; d < KX; ++d) kx[d] = (d < ndist) ? xa[d] : 0.0;
+#pragma unroll
+    for (int o2 = 0; o2 < NY; ++o2) ky[o2] = srec[P.off_y + o2];
     // P-chain multipliers: A column j (state lanes), B column c (Markov lanes)
     double mP[NS];
     if (st) {
-      const double* src = rec + P.off_A + j;
+      const double* src = srec + P.off_A + j;
 #pragma unroll
       for (int l = 0; l < NS; ++l) mP[l] = src[l * NS];
     } else if (mk) {
-      const double* src = rec + P.off_B + cm;
+      const double* src = srec + P.off_B + cm;
 #pragma unroll
       for (int l = 0; l < NS; ++l) mP[l] = src[l * NUT];
     } else {
 #pragma unroll
       for (int l = 0; l < NS; ++l) mP[l] = 0.0;
     }
-    // delay-line inputs w_t of the QP, AdjustAllDelayedStates applied
-    // (include/aug_lin_sys.h:141-154); zero once the line has drained
-    {
-      const double* xa = rec + P.off_x;
-#pragma unroll
-      for (int k = 0; k < ND; ++k) {
-        const double uo = P.u_old[(size_t)qq * NUT + dinp[k]];
-        double* wk = wtab + (R * ND + k) * WL;
-        for (int t = j; t < WL; t += 16) {
-          double v = 0.0;
-          if (t < dlen[k]) v = ((t == 0) ? xa[ndist + k] : xa[boff[k] + t - 1]) - uo;
-          wk[t] = v;
-        }
-      }
-    }
-    // simulation multipliers and chain initialisation
-    double mS[NS + NDW];
-    double base = 0.0, pS = 0.0, yh = 0.0;
-    const double* yp = zeros;
-    int yinc = 0;
+    // simulation multipliers of the state lanes: A row j, Adelay columns
+    double mS[NS + NDW], fj = 0.0;
     if (st) {
-      const double* arow = rec + P.off_A + j * NS;
-      const double* brow = rec + P.off_B + j * NUT;
+      const double* arow = srec + P.off_A + j * NS;
+      const double* brow = srec + P.off_B + j * NUT;
 #pragma unroll
       for (int l = 0; l < NS; ++l) mS[l] = arow[l];
 #pragma unroll
       for (int k = 0; k < NDW; ++k) mS[NS + k] = (ND > 0) ? brow[dinp[k]] : 0.0;
-      base = rec[P.off_f + j];
+      fj = srec[P.off_f + j];
+    } else {
+#pragma unroll
+      for (int l = 0; l < NS + NDW; ++l) mS[l] = 0.0;
+    }
+    // every staged read is issued before the first table write below (LDS
+    // operations of a wave execute in order)
+    __builtin_amdgcn_sched_barrier(0);
+    // restore the zero areas the staging overwrote: the m - 1 history entries
+    // at the head of each delayed input's line, and the zero slots
+#pragma unroll
+    for (int c = 0; c < NUT; ++c)
+      if (P.delay[c] > 0 && j < (M - 1) * NY) qlines[P.rows.lo[c] + j] = 0.0;
+    if (j < U * NY) qlines[P.rows.zr_off + j] = 0.0;
+
+    // C_hat = L_W' C_sel (ny x nobs): lane j computes column j of its QP
+    double pP[NY];
+#pragma unroll
+    for (int o = 0; o < NY; ++o) {
+      double t = 0.0;
+#pragma unroll
+      for (int o2 = 0; o2 < NY; ++o2)
+        if (o2 >= o) t += lwt[o * NY + o2] * cs[o2];
+      if (j < nobs) chq[o * 16 + j] = t;
+      pP[o] = st ? t : 0.0;  // P_0 = C_hat[:, :ns]
+    }
+    // delay-line inputs of the QP, AdjustAllDelayedStates applied
+    // (include/aug_lin_sys.h:141-154); zero once the line has drained
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      double* wk = wtab + (R * ND + k) * WL;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = j + 16 * i;
+        if (t < WL) wk[t] = (t < dlen[k]) ? xw[k][i] - uo[k] : 0.0;
+      }
+      const double* gxa = P.lin + (size_t)qq * rec_len + P.off_x;  // long horizons only
+      for (int t = j + 64; t < WL; t += 16) wk[t] = (t < dlen[k]) ? gxa[boff[k] + t - 1] - uo[k] : 0.0;
+    }
+    // simulation chain initialisation
+    double base = 0.0, pS = 0.0, yh = 0.0;
+    const double* yp = zeros;
+    int yinc = 0;
+    if (st) {
+      base = fj;
       pS = base;
 #pragma unroll
       for (int k = 0; k < ND; ++k) pS += mS[NS + k] * wtab[(R * ND + k) * WL];  // x_1 = f + Adelay w_0
     } else if (ol) {
 #pragma unroll
       for (int l = 0; l < NS; ++l) mS[l] = chq[oo * 16 + l];
-#pragma unroll
-      for (int k = 0; k < NDW; ++k) mS[NS + k] = 0.0;
       // kappa = L_W'(dist + y_prev) = C_hat_dist xa_dist + L_W' y_prev
       double t = 0.0;
-      for (int d = 0; d < ndist; ++d) t += chq[oo * 16 + NS + d] * rec[P.off_x + d];
+#pragma unroll
+      for (int d = 0; d < KX; ++d)
+        if (d < ndist) t += chq[oo * 16 + NS + d] * kx[d];
 #pragma unroll
       for (int o2 = 0; o2 < NY; ++o2)
-        if (o2 >= oo) t += lwt[oo * NY + o2] * rec[P.off_y + o2];
+        if (o2 >= oo) t += lwt[oo * NY + o2] * ky[o2];
       base = t;
       const double* yl = ylT + (s * NY + oo) * yls;
       yh = yl[0];
       yp = yl + 1;
       yinc = 1;
-    } else {
-#pragma unroll
-      for (int l = 0; l < NS + NDW; ++l) mS[l] = 0.0;
-      if (cl) {
-        const double* wk = wtab + (R * ND + kc) * WL;
-        pS = wk[1];
-        yh = wk[2];
-        yp = wk + 3;
-        yinc = 1;
-      }
+    } else if (cl) {
+      const double* wk = wtab + (R * ND + kc) * WL;
+      pS = wk[1];
+      yh = wk[2];
+      yp = wk + 3;
+      yinc = 1;
     }
     // ring history before t = 0
     if (tl) {

@@ -99,6 +99,7 @@ struct cmpc_ctx {
   int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
   // build kernel selection (cmpc_set_build_variant)
   int build_variant = CMPC_BUILD_AUTO;
+  int last_build = 0;  // kernel launched by the last cmpc_build
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
@@ -1063,6 +1064,11 @@ int cmpc_set_build_variant(cmpc_ctx* c, int variant) {
   return 0;
 }
 
+int cmpc_last_build_kernel(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  return c->last_build;
+}
+
 int cmpc_build(cmpc_ctx* c) {
   if (!c) return fail("null context");
   if (ensure_cfg(c)) return -1;
@@ -1115,7 +1121,7 @@ int cmpc_build(cmpc_ctx* c) {
     P.cus = cus;
     P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
   }
-  cmpc_rows_layout(d, L.nd, L.nobs, &P.rows);  // cached per dimension set
+  cmpc_rows_layout(d, L.nd, L.nobs, L.rec_len, &P.rows);  // cached per dimension set
   hipEvent_t e0 = nullptr;
   if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
   int rc = -1;
@@ -1128,8 +1134,12 @@ int cmpc_build(cmpc_ctx* c) {
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)
     return fail("row-layout build kernel not available for these dimensions");
-  if (rc && cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
-    return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
+  c->last_build = CMPC_BUILD_ROWS;
+  if (rc) {
+    if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
+      return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
+    c->last_build = CMPC_BUILD_WAVE;
+  }
   if (check_launch("build kernel")) return -1;
   return timed_end(c, CMPC_KERNEL_BUILD, e0);
 }

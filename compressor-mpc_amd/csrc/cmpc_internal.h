@@ -161,7 +161,7 @@ int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
                            void* stream);
 // LDS layout of the row kernel, chosen by a bank-conflict model of its
 // horizon loop (rows_layout.cpp); cached per dimension set, thread-safe.
-void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out);
+void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out);
 // modelled extra LDS cycles per wave-step of the horizon loop for one wave
 double cmpc_rows_layout_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave);
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,

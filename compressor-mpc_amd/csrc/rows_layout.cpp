@@ -32,6 +32,7 @@ namespace {
 
 constexpr int kU = 4;             // horizon unroll of the kernel (U in build_rows.hip)
 constexpr int kLdsBytes = 160 * 1024;
+constexpr int kWgPerCu = 3;       // resident workgroups per CU the kernel's VGPRs allow
 
 struct Pads {
   int order[CMPC_MAX_INPUTS];
@@ -43,7 +44,7 @@ int up(int v, int a) { return (v + a - 1) / a * a; }
 
 // The layout for given paddings (all offsets in doubles).  Returns the LDS
 // bytes per workgroup.
-size_t make_layout(const cmpc_dims& d, int nd, const Pads& pd, RowsLayout* R) {
+size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, RowsLayout* R) {
   std::memset(R, 0, sizeof *R);
   const int M = d.m, ny = d.ny, U = kU;
   int o = 0;
@@ -66,7 +67,8 @@ size_t make_layout(const cmpc_dims& d, int nd, const Pads& pd, RowsLayout* R) {
   R->ch_off = 4 * R->LQ;
   R->w_off = R->ch_off + 4 * ny * 16 + pd.w;
   R->WL = up(d.p + 2 + U, 2) + pd.WL;
-  R->per_wave = up(R->w_off + 4 * nd * R->WL, 2);
+  // the group's four records are staged over the wave's region first
+  R->per_wave = std::max(up(R->w_off + 4 * nd * R->WL, 2), up(4 * rec_len, 2));
   R->yls = d.p + U + pd.yls;
   R->yl_off = 16 + pd.yl;
   R->lw_off = R->yl_off + d.S * ny * R->yls;
@@ -229,12 +231,12 @@ uint64_t lcg(uint64_t& s) {
 
 }  // namespace
 
-void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out) {
+void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out) {
   std::memset(out, 0, sizeof *out);
   if (d.m < 1 || d.m > 2 || nobs > 16) return;
   static std::mutex mu;
   static std::map<std::vector<int>, RowsLayout> cache;
-  std::vector<int> key{d.ns, d.ny, d.nu, d.nu_tot, d.m, d.p, d.S, nd, nobs};
+  std::vector<int> key{d.ns, d.ny, d.nu, d.nu_tot, d.m, d.p, d.S, nd, nobs, rec_len};
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) key.push_back(d.delay[c]);
   {
     std::lock_guard<std::mutex> lk(mu);
@@ -247,15 +249,16 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out) {
   Pads base{};
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
   RowsLayout best;
-  const size_t base_bytes = make_layout(d, nd, base, &best);
+  const size_t base_bytes = make_layout(d, nd, rec_len, base, &best);
   // CMPC_ROWS_LAYOUT=packed: regions back to back (diagnostic A/B timing)
   const char* env = std::getenv("CMPC_ROWS_LAYOUT");
   const bool packed = env && std::strcmp(env, "packed") == 0;
   if (packed) {
     best.ok = base_bytes <= (size_t)kLdsBytes;
   } else if (base_bytes <= (size_t)kLdsBytes) {
-    // keep the workgroups per CU of the packed layout
-    const int wg = (int)(kLdsBytes / base_bytes);
+    // keep the workgroups per CU of the packed layout (at most kWgPerCu: the
+    // kernel's register budget, amdgpu_waves_per_eu(3) with 4 waves each)
+    const int wg = std::min(kWgPerCu, (int)(kLdsBytes / base_bytes));
     const size_t budget = (size_t)(kLdsBytes / wg) / 512 * 512;
     double best_cost = loop_conflicts(d, nd, best, 0);
     Pads bp = base;
@@ -276,7 +279,7 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out) {
         for (int i = d.nu_tot - 1; i > 0; --i) std::swap(cand.order[i], cand.order[lcg(seed) % (i + 1)]);
       }
       RowsLayout R;
-      if (make_layout(d, nd, cand, &R) > budget) continue;
+      if (make_layout(d, nd, rec_len, cand, &R) > budget) continue;
       const double cost = loop_conflicts(d, nd, R, 0);
       if (cost < best_cost) {
         best_cost = cost;
@@ -284,7 +287,7 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, RowsLayout* out) {
         bp = cand;
       }
     }
-    best.ok = make_layout(d, nd, bp, &best) <= (size_t)kLdsBytes;
+    best.ok = make_layout(d, nd, rec_len, bp, &best) <= (size_t)kLdsBytes;
   }
   std::lock_guard<std::mutex> lk(mu);
   cache[key] = best;
@@ -301,12 +304,12 @@ extern "C" int cmpc_rows_lds_model(const cmpc_dims* d, double* packed_cycles, do
   cmpc_layout L;
   if (cmpc_layout_of(d, &L)) return -1;
   RowsLayout R;
-  cmpc_rows_layout(*d, L.nd, L.nobs, &R);
+  cmpc_rows_layout(*d, L.nd, L.nobs, L.rec_len, &R);
   if (!R.ok) return -1;
   Pads base{};
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
   RowsLayout P0;
-  make_layout(*d, L.nd, base, &P0);
+  make_layout(*d, L.nd, L.rec_len, base, &P0);
   if (packed_cycles) *packed_cycles = loop_conflicts(*d, L.nd, P0, 0);
   if (chosen_cycles) *chosen_cycles = loop_conflicts(*d, L.nd, R, 0);
   if (lds_bytes)

@@ -153,6 +153,9 @@ int cmpc_build(cmpc_ctx* ctx);
 #define CMPC_BUILD_WAVE 1
 #define CMPC_BUILD_ROWS 2
 int cmpc_set_build_variant(cmpc_ctx* ctx, int variant);
+/* The build kernel the last cmpc_build launched (CMPC_BUILD_WAVE or
+ * CMPC_BUILD_ROWS), 0 before the first build, <0 on a null context. */
+int cmpc_last_build_kernel(cmpc_ctx* ctx);
 /* Diagnostic (no GPU needed): the row kernel's LDS layout for *dims as
  * cmpc_build chooses it.  Writes the bank-conflict model's extra LDS cycles
  * per wave-step of the horizon loop (wave 0) for the packed layout (regions

@@ -98,4 +98,4 @@ def test_rows_lds_layout_search(plant, ctype, p):
     assert 0 < nbytes <= 160 * 1024
     if (plant, ctype, p) == ("par", "coop", 50):
         assert packed > 20 and chosen <= 3.0
-        assert 160 * 1024 // nbytes == 4  # still four workgroups (16 waves) per CU
+        assert 160 * 1024 // nbytes >= 3  # the kernel runs three 4-wave workgroups per CU

@@ -66,9 +66,10 @@ def main():
                     e[c + "_frac"] = d[c] / d["SQ_WAVE_CYCLES"]
         summary["kernels"][k] = e
     json.dump(summary, open(os.path.join(PROF, f"{rnd}_pmc.json"), "w"), indent=1)
-    b = summary["kernels"].get("cmpc_build_kernel", {})
+    bk = "cmpc_build_rows_kernel" if "cmpc_build_rows_kernel" in summary["kernels"] else "cmpc_build_kernel"
+    b = summary["kernels"].get(bk, {})
     if "hbm_bytes_per_launch" in b:
-        json.dump({"batch": batch, "round": rnd, "kernel": "cmpc_build_kernel",
+        json.dump({"batch": batch, "round": rnd, "kernel": bk,
                    "hbm_bytes_per_launch": b["hbm_bytes_per_launch"],
                    "hbm_read_bytes": b["hbm_read_bytes"], "hbm_write_bytes": b["hbm_write_bytes"],
                    "source": f"profiles/{rnd}_pmc.json"},

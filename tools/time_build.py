@@ -24,7 +24,7 @@ for p in PS:
             for _ in range(3): ctx.build()
             ctx.synchronize()
             ctx.enable_timing(True)
-            for _ in range(10): ctx.build()
+            for _ in range(40): ctx.build()
             ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
             name = "wave" if v == cmpc.CMPC_BUILD_WAVE else "rows"
             print(f"p={p:4d}  {name} build {ms/n:.4f} ms  per QP-step {ms/n*1e6/(B*cfg.S*p):.3f} ns"
