@@ -54,6 +54,21 @@
 #ifndef CMPC_RX
 #define CMPC_RX 0
 #endif
+// Diagnostic build (tools/rows_timing.py): per-wave s_memtime cycle totals of
+// the group phases, written over the QP output (results invalid).
+#ifndef CMPC_ROWS_TIMING
+#define CMPC_ROWS_TIMING 0
+#endif
+#if CMPC_ROWS_TIMING
+#define CMPC_T(i)                                          \
+  {                                                        \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();    \
+    tsum[i] += now_ - tlast;                               \
+    tlast = now_;                                          \
+  }
+#else
+#define CMPC_T(i)
+#endif
 
 template <int NS, int NY, int NUT, int NU, int M, int ND>
 __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
@@ -148,9 +163,16 @@ void cmpc_build_rows_kernel(BuildParams P) {
   const int wsw = (wdel && pp - dm > 0) ? pp - dm : -1;
   const bool tl = M > 1 && mk && dm == 0;  // ring writer: copies each group's last value to entry -1
   double* const tq = qlines + lom;
-  double* const zq = qlines + P.rows.z_off + oo;
+  // every lane stores each step (no exec-mask branches in the loop): lanes
+  // without a Markov or free-response role store into the dump area
+  double* const zq = ol ? qlines + P.rows.z_off + oo : dump;
 
+#if CMPC_ROWS_TIMING
+  uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  int ngrp = 0;
+#endif
   for (int g = blockIdx.x * CMPC_BUILD_WAVES + wave; g < ngroups; g += nwaves) {
+    CMPC_T(5)  // loop back-edge / tail of the previous group
     const int q = 4 * g + R;
     const bool qv = q < nqp;
     const int qq = qv ? q : nqp - 1;
@@ -179,7 +201,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
     double uo[NDW];
 #pragma unroll
     for (int k = 0; k < NDW; ++k) uo[k] = (k < ND) ? P.u_old[(size_t)qq * NUT + dinp[k]] : 0.0;
+    CMPC_T(0)  // staging issue
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    CMPC_T(1)  // staging wait
     const double* srec = wreg + R * rec_len;  // this row's record (staged)
     const double* xa = srec + P.off_x;
     double xw[NDW][4];  // delay-line sources of w_t, t = j + 16 i < 64
@@ -341,10 +365,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
     _Pragma("unroll") for (int o = 0; o < NY; ++o) pP[o] = aP[o];           \
     pS = aS;                                                                \
     if (CMPC_RX != 1 && CMPC_RX != 4) {                                     \
-      if (mk) {                                                             \
-        _Pragma("unroll") for (int o = 0; o < NY; ++o) wq[(u) * NY + o] = aP[o]; \
-      }                                                                     \
-      if (ol) zq[(u) * NY] = aS;                                            \
+      _Pragma("unroll") for (int o = 0; o < NY; ++o) wq[(u) * NY + o] = aP[o]; \
+      zq[(u) * NY] = aS;                                                    \
     }                                                                       \
     if (CMPC_RX != 1) {                                                     \
       _Pragma("unroll") for (int o = 0; o < NY; ++o) rd[o] = rq[(u) * NY + o]; \
@@ -356,6 +378,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     _Pragma("unroll") for (int o = 0; o < NY; ++o) tq[o] = pP[o];           \
   }
 
+    CMPC_T(2)  // prologue compute
     int r = 0;
     for (int sg = 0; sg <= nseg; ++sg) {
       int r_end = pp;
@@ -388,8 +411,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
     for (int o = 0; o < NY; ++o) cv[o] = __builtin_fma(smask, cv[o], rd[o]);
     rows_gacc<NY, NUT, NU, M>(cv, acc);  // row p - 1
     asm volatile("" ::"v"(pf0), "v"(pf1));
+    CMPC_T(3)  // horizon loop
 
-    if (qv && gl) {
+    if (qv && gl && !CMPC_ROWS_TIMING) {
       double* out = P.qp + (size_t)q * P.qp_len;
       constexpr int nuo = NUT - NU, nVo = M * nuo;
       const double* uwt = uw_all + s * NU * NU;
@@ -409,7 +433,19 @@ void cmpc_build_rows_kernel(BuildParams P) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    CMPC_T(4)  // epilogue
+#if CMPC_ROWS_TIMING
+    ++ngrp;
+#endif
   }
+#if CMPC_ROWS_TIMING
+  if (lane == 0) {
+    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 8;
+    for (int i = 0; i < 6; ++i) dbg[i] = (double)tsum[i];
+    dbg[6] = ngrp;
+    dbg[7] = 1.0;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -1129,7 +1129,7 @@ int cmpc_build(cmpc_ctx* c) {
   // (at one workgroup, i.e. one wave per SIMD, the one-QP-per-wave kernel is
   // faster: coop p = 100 measured 0.94 vs 0.86 ms)
   const size_t rows_lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * CMPC_BUILD_WAVES);
-  const bool rows_auto = rows_lds <= 80 * 1024;
+  const bool rows_auto = (160 * 1024 / rows_lds) * CMPC_BUILD_WAVES >= 8;  // >= 8 waves per CU
   if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_auto))
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)

@@ -1,0 +1,32 @@
+"""Per-phase cycle attribution of the row build kernel (diagnostic library
+built with -DCMPC_ROWS_TIMING=1: tools/ablate/libcmpc_timing.so).
+usage: CMPC_LIBRARY=.../libcmpc_timing.so python tools/rows_timing.py [p]"""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
+import numpy as np
+import cmpc
+from cmpc.configs import reference_setup
+from cmpc.synthetic import synthetic_batch
+p = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+B = 65536
+cfg = cmpc.reference_config("par", "coop", p=p)
+arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
+with cmpc.Context(cfg, B) as ctx:
+    ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
+    ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
+    for _ in range(5):
+        ctx.build()
+    ctx.synchronize()
+    H, f, G = ctx.download_qp()
+raw = np.concatenate([H.reshape(H.shape[0], -1), f, G.reshape(G.shape[0], -1)], axis=1).reshape(-1)
+d = raw[: (raw.size // 8) * 8].reshape(-1, 8)
+d = d[d[:, 7] == 1.0]
+ng = d[:, 6].sum()
+names = ["tail/back-edge", "staging issue", "staging wait", "prologue compute", "horizon loop", "epilogue"]
+order = [5, 0, 1, 2, 3, 4]
+tot = d[:, :6].sum()
+print(f"p={p}: {len(d)} waves, {ng:.0f} groups; s_memtime cycles per group:")
+for i in order:
+    print(f"  {names[order.index(i)] if False else ['staging issue','staging wait','prologue compute','horizon loop','epilogue','tail/back-edge'][i]:18s} {d[:, i].sum() / ng:10.0f}  ({d[:, i].sum() / tot * 100:5.1f} %)")
