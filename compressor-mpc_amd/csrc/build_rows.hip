@@ -169,10 +169,26 @@ void cmpc_build_rows_kernel(BuildParams P) {
 
 #if CMPC_ROWS_TIMING
   uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  const uint64_t t0c = tlast, t0r = __builtin_amdgcn_s_memrealtime();
   int ngrp = 0;
 #endif
+  // Fair progress.  The SIMD issues from its oldest ready wave first, so with
+  // a static group assignment the oldest wave finished early and the youngest
+  // ran alone at the end (wave lifetimes 0.19-0.35 ms for a 0.35 ms kernel,
+  // tools/rows_timing.py).  Each wave lowers its issue priority as it
+  // completes quarters of its share, so waves that are behind win arbitration.
+  const int share = (ngroups + nwaves - 1) / nwaves;
+  int done_groups = 0;
+  __builtin_amdgcn_s_setprio(3);
   for (int g = blockIdx.x * CMPC_BUILD_WAVES + wave; g < ngroups; g += nwaves) {
     CMPC_T(5)  // loop back-edge / tail of the previous group
+    {
+      const int level = 3 - (4 * done_groups) / share;  // 3 .. 0
+      if (level <= 0) __builtin_amdgcn_s_setprio(0);
+      else if (level == 1) __builtin_amdgcn_s_setprio(1);
+      else if (level == 2) __builtin_amdgcn_s_setprio(2);
+      ++done_groups;
+    }
     const int q = 4 * g + R;
     const bool qv = q < nqp;
     const int qq = qv ? q : nqp - 1;
@@ -440,10 +456,15 @@ void cmpc_build_rows_kernel(BuildParams P) {
   }
 #if CMPC_ROWS_TIMING
   if (lane == 0) {
-    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 8;
+    const uint64_t t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
+    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 16;
     for (int i = 0; i < 6; ++i) dbg[i] = (double)tsum[i];
     dbg[6] = ngrp;
     dbg[7] = 1.0;
+    dbg[8] = (double)(t1c - t0c);  // shader cycles of the wave's lifetime
+    dbg[9] = (double)(t1r - t0r);  // 100 MHz ticks of the same span
+    dbg[10] = (double)t0r;
+    dbg[11] = (double)t1r;
   }
 #endif
 }

@@ -21,7 +21,7 @@ with cmpc.Context(cfg, B) as ctx:
     ctx.synchronize()
     H, f, G = ctx.download_qp()
 raw = np.concatenate([H.reshape(H.shape[0], -1), f, G.reshape(G.shape[0], -1)], axis=1).reshape(-1)
-d = raw[: (raw.size // 8) * 8].reshape(-1, 8)
+d = raw[: (raw.size // 16) * 16].reshape(-1, 16)
 d = d[d[:, 7] == 1.0]
 ng = d[:, 6].sum()
 names = ["tail/back-edge", "staging issue", "staging wait", "prologue compute", "horizon loop", "epilogue"]
@@ -30,3 +30,10 @@ tot = d[:, :6].sum()
 print(f"p={p}: {len(d)} waves, {ng:.0f} groups; s_memtime cycles per group:")
 for i in order:
     print(f"  {names[order.index(i)] if False else ['staging issue','staging wait','prologue compute','horizon loop','epilogue','tail/back-edge'][i]:18s} {d[:, i].sum() / ng:10.0f}  ({d[:, i].sum() / tot * 100:5.1f} %)")
+clk = d[:, 8] / (d[:, 9] / 100e6) / 1e9
+print(f"  in-kernel shader clock: median {np.median(clk):.3f} GHz (min {clk.min():.3f}, max {clk.max():.3f})")
+st, en = d[:, 10], d[:, 11]
+span = (en.max() - st.min()) / 100e6 * 1e3
+print(f"  kernel span (first wave start -> last wave end): {span:.4f} ms; wave lifetime ms: "
+      f"min {d[:, 9].min() / 1e5:.4f} median {np.median(d[:, 9]) / 1e5:.4f} max {d[:, 9].max() / 1e5:.4f}; "
+      f"start skew max {(st.max() - st.min()) / 1e5:.4f} ms")
