@@ -54,6 +54,12 @@
 #ifndef CMPC_RX
 #define CMPC_RX 0
 #endif
+#ifndef CMPC_ROWS_PF
+#define CMPC_ROWS_PF 0  // L2 prefetch of the next group's records (2% slower with LDS staging)
+#endif
+#ifndef CMPC_ROWS_PRIO
+#define CMPC_ROWS_PRIO 1  // 1: priority by progress; 2: + prologue at top priority
+#endif
 // Diagnostic build (tools/rows_timing.py): per-wave s_memtime cycle totals of
 // the group phases, written over the QP output (results invalid).
 #ifndef CMPC_ROWS_TIMING
@@ -182,6 +188,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
   __builtin_amdgcn_s_setprio(3);
   for (int g = blockIdx.x * CMPC_BUILD_WAVES + wave; g < ngroups; g += nwaves) {
     CMPC_T(5)  // loop back-edge / tail of the previous group
+#if CMPC_ROWS_PRIO == 2
+    __builtin_amdgcn_s_setprio(3);  // latency-bound prologue first
+#else
     {
       const int level = 3 - (4 * done_groups) / share;  // 3 .. 0
       if (level <= 0) __builtin_amdgcn_s_setprio(0);
@@ -189,6 +198,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
       else if (level == 2) __builtin_amdgcn_s_setprio(2);
       ++done_groups;
     }
+#endif
     const int q = 4 * g + R;
     const bool qv = q < nqp;
     const int qq = qv ? q : nqp - 1;
@@ -348,12 +358,12 @@ void cmpc_build_rows_kernel(BuildParams P) {
     double* rq = r_start;
     int winc = winc0, rinc = 0;
 
-    // L2 prefetch of this wave's next group of records: one dword per
-    // 128-byte line, consumed (and so waited for) only after the horizon
-    // loop, before the output stores; the prologue of the next group then
-    // reads from L2 instead of HBM.
+    // Optional L2 prefetch of this wave's next group of records (one dword
+    // per 128-byte line, consumed after the horizon loop).  Off: since the
+    // records are staged with one LDS-DMA round trip, it only added HBM
+    // re-fetches (A/B: 0.328 vs 0.322 ms).
     float pf0 = 0.f, pf1 = 0.f;
-    if (CMPC_RX != 2) {
+    if (CMPC_ROWS_PF) {
       const int gn = g + nwaves;
       if (gn < ngroups) {
         const char* nb = reinterpret_cast<const char*>(P.lin + (size_t)4 * gn * rec_len);
@@ -395,6 +405,15 @@ void cmpc_build_rows_kernel(BuildParams P) {
   }
 
     CMPC_T(2)  // prologue compute
+#if CMPC_ROWS_PRIO == 2
+    {
+      const int level = 2 - (3 * done_groups) / share;  // 2 .. 0
+      if (level <= 0) __builtin_amdgcn_s_setprio(0);
+      else if (level == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(2);
+      ++done_groups;
+    }
+#endif
     int r = 0;
     for (int sg = 0; sg <= nseg; ++sg) {
       int r_end = pp;
