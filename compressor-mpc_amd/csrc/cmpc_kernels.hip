@@ -234,7 +234,20 @@ void cmpc_build_kernel(BuildParams P) {
   }
   double uold_l = (q < P.nqp && lane < NUT) ? P.u_old[(size_t)q * NUT + lane] : 0.0;
 
+  // fair progress of a SIMD's waves: priority drops per completed quarter of
+  // the wave's share (the SIMD otherwise favours its oldest wave and the
+  // kernel waits on the youngest; cf. build_rows.hip)
+  const int share = (P.nqp + nwaves - 1) / nwaves;
+  int done_qp = 0;
+  __builtin_amdgcn_s_setprio(3);
   for (; q < P.nqp; q += nwaves) {
+    {
+      const int level = 3 - (4 * done_qp) / share;
+      if (level <= 0) __builtin_amdgcn_s_setprio(0);
+      else if (level == 1) __builtin_amdgcn_s_setprio(1);
+      else if (level == 2) __builtin_amdgcn_s_setprio(2);
+      ++done_qp;
+    }
     const int s = q % S;
     const double* yl = yl_all + s * P.yl_stride;
     const double* lwt = lw_all + s * NY * NY;
