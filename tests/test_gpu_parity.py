@@ -320,3 +320,20 @@ def test_gpu_survey_config(plant, ctype, p, B, K):
     odu, ost, *_ = O.step(sub, arr, lin_s, K, u_s.copy(), np.zeros((len(qs), n)),
                           np.zeros(len(qs), np.uint32), init=True)
     np.testing.assert_allclose(du[qs], odu, rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p,expect", [(50, "rows"), (100, "wave")])
+def test_gpu_build_auto_selects_kernel(p, expect):
+    """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel where its LDS leaves
+    >= 2 workgroups per CU (coop p = 50) and the one-QP-per-wave kernel past
+    that (coop p = 100); DESIGN.md §3.0."""
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=p)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 64
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=5)
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.build()
+        got = ctx.last_build_kernel()
+    assert got == {"rows": cmpc.CMPC_BUILD_ROWS, "wave": cmpc.CMPC_BUILD_WAVE}[expect]

@@ -10,6 +10,12 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 9
 cfg = cmpc.reference_config("par", "coop", p=50)
 arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
 lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=2048)
+if os.environ.get("CMPC_TI_UNCONSTRAINED"):  # diagnostic: bounds far away, no active set
+    import numpy as np
+    for s_ in range(cfg.S):
+        arr.lower[s_][:] = -1e6; arr.upper[s_][:] = 1e6
+        arr.rate_lower[s_][:] = -1e6; arr.rate_upper[s_][:] = 1e6
+    ws = np.zeros_like(ws)
 with cmpc.Context(cfg, B) as ctx:
     ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
     ctx.build(); ctx.init_warmstart()
