@@ -1125,12 +1125,11 @@ int cmpc_build(cmpc_ctx* c) {
   hipEvent_t e0 = nullptr;
   if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
   int rc = -1;
-  // AUTO: the row kernel while its LDS allows two or more workgroups per CU
-  // (at one workgroup, i.e. one wave per SIMD, the one-QP-per-wave kernel is
-  // faster: coop p = 100 measured 0.94 vs 0.86 ms)
-  const size_t rows_lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * CMPC_BUILD_WAVES);
-  const bool rows_auto = (160 * 1024 / rows_lds) * CMPC_BUILD_WAVES >= 8;  // >= 8 waves per CU
-  if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_auto))
+  // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
+  // than the one-QP-per-wave kernel for every plant/controller type at
+  // p = 20, 50, 100: tools/gpu_config_sweep.sh), else the
+  // one-QP-per-wave kernel (e.g. cent p = 200)
+  if (c->build_variant == CMPC_BUILD_ROWS || c->build_variant == CMPC_BUILD_AUTO)
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)
     return fail("row-layout build kernel not available for these dimensions");

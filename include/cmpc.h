@@ -147,8 +147,7 @@ int cmpc_build(cmpc_ctx* ctx);
 /* Build-kernel selection for cmpc_build (same H, f, G within rounding):
  * CMPC_BUILD_ROWS four QPs per wave, one per 16-lane DPP row (m <= 2, LDS
  * fits); CMPC_BUILD_WAVE one QP per wave (every instantiated dimension set);
- * CMPC_BUILD_AUTO (default) rows where its LDS leaves >= 2 workgroups per CU,
- * else wave. */
+ * CMPC_BUILD_AUTO (default) rows where its LDS fits, else wave. */
 #define CMPC_BUILD_AUTO 0
 #define CMPC_BUILD_WAVE 1
 #define CMPC_BUILD_ROWS 2

@@ -323,13 +323,13 @@ def test_gpu_survey_config(plant, ctype, p, B, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,expect", [(50, "rows"), (100, "wave")])
-def test_gpu_build_auto_selects_kernel(p, expect):
-    """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel where its LDS leaves
-    >= 2 workgroups per CU (coop p = 50) and the one-QP-per-wave kernel past
-    that (coop p = 100); DESIGN.md §3.0."""
-    _, setup, _, _ = setup_for("par", "coop")
-    cfg = cmpc.reference_config("par", "coop", p=p)
+@pytest.mark.parametrize("ctype,p,expect", [("coop", 50, "rows"), ("coop", 100, "rows"),
+                                            ("cent", 200, "wave")])
+def test_gpu_build_auto_selects_kernel(ctype, p, expect):
+    """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel wherever its LDS fits
+    and the one-QP-per-wave kernel past that (cent p = 200); DESIGN.md §3.0."""
+    _, setup, _, _ = setup_for("par", ctype)
+    cfg = cmpc.reference_config("par", ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
     B = 64
     lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=5)
