@@ -464,6 +464,9 @@ void cmpc_build_kernel(BuildParams P) {
 
 #include "qp_solver.h"
 
+#ifndef CMPC_SOLVE_WPE
+#define CMPC_SOLVE_WPE(N) ((N) >= 6 ? 1 : 2)
+#endif
 #ifndef CMPC_SOLVE_PRIO
 #define CMPC_SOLVE_PRIO 1  // priority by Jacobi-iteration progress (iterate 0.049 -> 0.047 ms)
 #endif
@@ -480,8 +483,15 @@ struct HinvLds {
 // Jacobi iterate kernel (lane per QP)
 // ---------------------------------------------------------------------------
 template <int N, int NU, int NVO>
-__global__ __launch_bounds__(CMPC_SOLVE_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ __launch_bounds__(CMPC_SOLVE_THREADS)
+__attribute__((amdgpu_waves_per_eu(CMPC_SOLVE_WPE(N), CMPC_SOLVE_WPE(N))))
 void cmpc_solve_kernel(SolveParams P) {
+  // nV >= 6 (centralized, m = 3): one wave per SIMD with the AGPR half of the
+  // register file open for spills (an AGPR clobber keeps the compiler from
+  // inferring "no AGPRs"): nV = 8 scratch 1480 -> 464 B per lane, iterate
+  // (K = 1, 65 536 centralized QPs) 0.131 -> 0.049 ms.  nV = 4 stays at two
+  // waves per SIMD (one wave measured 0.073 vs 0.048 ms)
+  if constexpr (CMPC_SOLVE_WPE(N) == 1) asm volatile("" ::: "a0");
   constexpr int M = N / NU;
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
