@@ -451,6 +451,9 @@ int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
     if (hipPointerGetAttributes(&a, lin_device) != hipSuccess || a.type != hipMemoryTypeDevice ||
         a.device != c->device)
       return fail("cmpc_bind_lin: not a device pointer on the context's device");
+    // the build kernels read records with 16-byte loads (LDS-DMA / double2)
+    if (reinterpret_cast<uintptr_t>(lin_device) % 16 != 0)
+      return fail("cmpc_bind_lin: records must be 16-byte aligned");
   }
   c->lin_bound = lin_device;
   return 0;

@@ -138,8 +138,9 @@ void* cmpc_lin_device(cmpc_ctx* ctx);
  * e.g. to inspect what cmpc_produce_lin wrote. */
 int cmpc_download_lin(cmpc_ctx* ctx, double* lin_host);
 /* Bind an external device-resident record array (B*S*rec_len doubles on the
- * ctx device, e.g. the output of a device-side producer); NULL re-binds the
- * context's own buffer.  Takes effect for the next cmpc_build. */
+ * ctx device, 16-byte aligned, e.g. the output of a device-side producer);
+ * NULL re-binds the context's own buffer.  Takes effect for the next
+ * cmpc_build. */
 int cmpc_bind_lin(cmpc_ctx* ctx, const double* lin_device);
 
 /* Hot path. */
