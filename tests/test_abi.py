@@ -99,3 +99,18 @@ def test_rows_lds_layout_search(plant, ctype, p):
     if (plant, ctype, p) == ("par", "coop", 50):
         assert packed > 20 and chosen <= 3.0
         assert 160 * 1024 // nbytes >= 3  # the kernel runs three 4-wave workgroups per CU
+
+
+def test_rows_lds_model_python_mirror_agrees():
+    """tools/lds_rows_sim.py (the model in Python) and the library's model
+    (rows_layout.cpp) give the same conflicts and LDS bytes for the packed
+    layout of the bench configuration."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import lds_rows_sim as sim
+    cfg = reference_config("par", "coop", p=50)
+    dims = CmpcDims.from_config(cfg, 8)
+    packed, _, _ = cmpc.rows_lds_model(dims)
+    d = dict(sim.PAR_COOP, p=50)
+    L = sim.layout(d)
+    assert abs(sim.simulate(d, L, 0)[1] - packed) < 1e-9

@@ -21,7 +21,7 @@ def up(v, a):
 
 
 def layout(d, over=None):
-    """Mirror of build_rows_layout (cmpc_abi.cpp); `over` may override
+    """Mirror of make_layout (rows_layout.cpp); `over` may override
     region offsets/paddings (doubles)."""
     over = over or {}
     M, ny, p = d["m"], d["ny"], d["p"]
@@ -46,10 +46,12 @@ def layout(d, over=None):
     L["zr_off"] = o
     o += U * ES
     L["LQ"] = up(o, 2) + over.get("pad_LQ", 0)
+    # wave region [lines 4 x LQ][C_hat 4 x ny x 16][w tables 4 x nd x WL], at
+    # least the four staged records (rows_layout.cpp make_layout)
     L["ch_off"] = 4 * L["LQ"]
     L["w_off"] = L["ch_off"] + 4 * ny * 16 + over.get("pad_w", 0)
     L["WL"] = up(p + 2 + U, 2) + over.get("pad_WL", 0)
-    L["per_wave"] = up(L["w_off"] + 4 * d["nd"] * L["WL"], 2) + over.get("pad_wave", 0)
+    L["per_wave"] = max(up(L["w_off"] + 4 * d["nd"] * L["WL"], 2), up(4 * d["rec_len"], 2)) + over.get("pad_wave", 0)
     L["yls"] = p + U + over.get("pad_yls", 0)
     L["yl_off"] = 16 + over.get("pad_yl", 0)
     L["lw_off"] = L["yl_off"] + d["S"] * ny * L["yls"]
@@ -63,7 +65,7 @@ def layout(d, over=None):
                 if 0 < v < p:
                     segs.add(v)
     L["seg"] = sorted(segs)
-    L["bytes"] = 8 * (L["lds_block"] + 4 * L["per_wave"])
+    L["bytes"] = 8 * (L["lds_block"] + 4 * L["per_wave"])  # 4 waves per workgroup
     return L
 
 
@@ -151,7 +153,8 @@ def simulate(d, L, wave=0, verbose=False):
             yp, yinc = wreg + L["w_off"] + (R * ND + kc) * L["WL"] + 3, 1
         else:
             yp, yinc = 0, 0
-        lanes.append(dict(mk=mk, ol=ol, zq=ql + L["z_off"] + oo, tl=(M > 1 and mk and dm == 0),
+        # every lane stores each step: lanes without the role into the dump area
+        lanes.append(dict(mk=mk, ol=ol, zq=(ql + L["z_off"] + oo) if ol else dump, tl=(M > 1 and mk and dm == 0),
                           tq=ql + L["lo"][cm], rq=rs, rinc=0, rline=rline, rsw=rsw,
                           wq=ws, winc=winc0, wsw=wsw, dump=dump, yp=yp, yinc=yinc))
     tot = defaultdict(int)
@@ -163,8 +166,8 @@ def simulate(d, L, wave=0, verbose=False):
         nsteps += 1
         c, i = read_b64([ln["yp"] + u for ln in lanes]); tot["yh"] += c; ideal["yh"] += i
         for o in range(NY):  # compiler: write2_b64 (o, o+1) + write_b64; modelled as b64 writes
-            c, i = write_b64([ln["wq"] + u * ES + o if ln["mk"] else None for ln in lanes]); tot["wmk"] += c; ideal["wmk"] += i
-        c, i = write_b64([ln["zq"] + u * ES if ln["ol"] else None for ln in lanes]); tot["wz"] += c; ideal["wz"] += i
+            c, i = write_b64([ln["wq"] + u * ES + o for ln in lanes]); tot["wmk"] += c; ideal["wmk"] += i
+        c, i = write_b64([ln["zq"] + u * ES for ln in lanes]); tot["wz"] += c; ideal["wz"] += i
         o = 0
         while o < NY:
             if o + 1 < NY:
@@ -205,7 +208,7 @@ def simulate(d, L, wave=0, verbose=False):
     return extra, sum(extra.values())
 
 
-PAR_COOP = dict(ns=11, ny=3, nu=2, nu_tot=4, m=2, nd=2, S=2, delay=[0, 40, 0, 40])
+PAR_COOP = dict(ns=11, ny=3, nu=2, nu_tot=4, m=2, nd=2, S=2, delay=[0, 40, 0, 40], rec_len=312)
 
 if __name__ == "__main__":
     p = int(sys.argv[1]) if len(sys.argv) > 1 else 50
