@@ -83,7 +83,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   constexpr int NV = NU * M;
   constexpr int NG = M * NUT + 1;  // gather lanes: QP columns (move k, input c), then z
   constexpr int NDW = ND > 0 ? ND : 1;
-  constexpr int U = 4;             // horizon-loop unroll (immediate LDS offsets)
+  constexpr int U = CMPC_ROWS_U;   // horizon-loop unroll (immediate LDS offsets)
   static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   const int lane = threadIdx.x & 63;
@@ -286,7 +286,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
 #pragma unroll
     for (int c = 0; c < NUT; ++c)
       if (P.delay[c] > 0 && j < (M - 1) * NY) qlines[P.rows.lo[c] + j] = 0.0;
-    if (j < U * NY) qlines[P.rows.zr_off + j] = 0.0;
+    for (int e = j; e < U * NY; e += 16) qlines[P.rows.zr_off + e] = 0.0;
 
     // C_hat = L_W' C_sel (ny x nobs): lane j computes column j of its QP
     double pP[NY];
@@ -425,6 +425,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
         CMPC_ROWS_STEP(1)
         CMPC_ROWS_STEP(2)
         CMPC_ROWS_STEP(3)
+#if CMPC_ROWS_U >= 5
+        CMPC_ROWS_STEP(4)
+#endif
         CMPC_ROWS_TAIL()
         wq += U * winc;
         rq += U * rinc;

@@ -7,6 +7,9 @@
 
 #define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
 #define CMPC_BUILD_WAVES 4       // waves per build workgroup (one QP per wave at a time)
+#ifndef CMPC_ROWS_U
+#define CMPC_ROWS_U 4            // horizon unroll of the row build kernel (4 or 5; 5 measured no faster)
+#endif
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 #define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
 

@@ -30,7 +30,7 @@
 
 namespace {
 
-constexpr int kU = 4;             // horizon unroll of the kernel (U in build_rows.hip)
+constexpr int kU = CMPC_ROWS_U;   // horizon unroll of the kernel (U in build_rows.hip)
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kWgPerCu = 3;       // resident workgroups per CU the kernel's VGPRs allow
 
