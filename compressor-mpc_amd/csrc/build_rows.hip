@@ -76,8 +76,8 @@
 #define CMPC_T(i)
 #endif
 
-template <int NS, int NY, int NUT, int NU, int M, int ND>
-__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
+template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG>
+__global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(3, 3)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -93,7 +93,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   const int LQ = P.rows.LQ, WL = P.rows.WL, yls = P.rows.yls;
   const int nqp = P.nqp;
   const int ngroups = (nqp + 3) / 4;
-  const int nwaves = gridDim.x * CMPC_BUILD_WAVES;
+  const int nwaves = gridDim.x * WPG;  // WPG waves per workgroup (launcher: 4, 2 or 1)
 
   double* zeros = smem;
   double* ylT = smem + P.rows.yl_off;  // [S][NY][yls]  L_W' y_ref, output-major
@@ -104,7 +104,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   double* chs = wreg + P.rows.ch_off;   // [4][NY][16]  C_hat rows
   double* wtab = wreg + P.rows.w_off;   // [4][ND][WL]  delay-line inputs w_t
 
-  const int nthr = 64 * CMPC_BUILD_WAVES;
+  const int nthr = 64 * WPG;
   for (int e = threadIdx.x; e < S * NY * yls; e += nthr) {
     const int ss = e / (NY * yls), rem = e - ss * NY * yls;
     const int o = rem / yls, r = rem - o * yls;
@@ -186,7 +186,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   const int share = (ngroups + nwaves - 1) / nwaves;
   int done_groups = 0;
   __builtin_amdgcn_s_setprio(3);
-  for (int g = blockIdx.x * CMPC_BUILD_WAVES + wave; g < ngroups; g += nwaves) {
+  for (int g = blockIdx.x * WPG + wave; g < ngroups; g += nwaves) {
     CMPC_T(5)  // loop back-edge / tail of the previous group
 #if CMPC_ROWS_PRIO == 2
     __builtin_amdgcn_s_setprio(3);  // latency-bound prologue first
@@ -479,7 +479,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
 #if CMPC_ROWS_TIMING
   if (lane == 0) {
     const uint64_t t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
-    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 16;
+    double* dbg = P.qp + (size_t)(blockIdx.x * WPG + wave) * 16;
     for (int i = 0; i < 6; ++i) dbg[i] = (double)tsum[i];
     dbg[6] = ngrp;
     dbg[7] = 1.0;
@@ -494,22 +494,33 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // ---------------------------------------------------------------------------
 // launcher — explicit instantiation list (cf. the reference's *_list.h)
 // ---------------------------------------------------------------------------
-#define ROWS_CASE(NS_, NY_, NU_, M_)                                                           \
-  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {          \
-    auto kern = cmpc_build_rows_kernel<NS_, NY_, 4, NU_, M_, 2>;                               \
-    const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block +                            \
-                                         (size_t)P.rows.per_wave * CMPC_BUILD_WAVES);          \
-    if (lds > 64 * 1024)                                                                       \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);         \
-    int per_cu = 0;                                                                            \
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * CMPC_BUILD_WAVES,     \
-                                                     lds) != hipSuccess || per_cu < 1)         \
-      per_cu = std::max<int>(1, (int)((160 * 1024) / lds));                                    \
-    const int need = std::max(1, ((P.nqp + 3) / 4 + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES); \
-    const int grid = std::max(1, std::min(need, P.cus * per_cu));                              \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * CMPC_BUILD_WAVES), lds, s, P);              \
-    return 0;                                                                                  \
+// Waves per workgroup (4, or 2 where that holds 1.5x the resident waves;
+// cmpc_rows_waves_per_group in rows_layout.cpp).
+template <int NS, int NY, int NU, int M, int WPG>
+static int rows_launch(const BuildParams& P, hipStream_t s) {
+  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG>;
+  const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * WPG);
+  if (lds > 160 * 1024) return -1;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPG, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
+  const int need = std::max(1, ((P.nqp + 3) / 4 + WPG - 1) / WPG);
+  const int grid = std::max(1, std::min(need, P.cus * per_cu));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPG), lds, s, P);
+  return 0;
+}
+
+#define ROWS_CASE(NS_, NY_, NU_, M_)                                                  \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
+    switch (cmpc_rows_waves_per_group(P.rows)) {                                      \
+      case 4: return rows_launch<NS_, NY_, NU_, M_, 4>(P, s);                         \
+      case 2: return rows_launch<NS_, NY_, NU_, M_, 2>(P, s);                         \
+      default: return -1;                                                             \
+    }                                                                                 \
   }
 
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {

@@ -162,6 +162,9 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
 // Row-layout build kernel (build_rows.hip); -1 when not instantiated / not usable.
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
                            void* stream);
+// Waves per workgroup the row kernel launches with for layout R (4, 2 or 1;
+// 0: does not fit) (build_rows.hip).
+int cmpc_rows_waves_per_group(const RowsLayout& R);
 // LDS layout of the row kernel, chosen by a bank-conflict model of its
 // horizon loop (rows_layout.cpp); cached per dimension set, thread-safe.
 void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out);

@@ -16,7 +16,7 @@
 // LDS cycles per wave-step at coop p = 50, which PMC confirmed
 // (SQ_LDS_BANK_CONFLICT ≈ 30 per wave-step).  A deterministic search over the
 // order of the per-input lines and a few doubles of padding between regions,
-// within the LDS budget that keeps the same number of workgroups per CU,
+// within the LDS budget that keeps the resident waves per CU of the packed layout,
 // brings the model to ≈ 2.
 #include <algorithm>
 #include <cstdint>
@@ -32,7 +32,6 @@ namespace {
 
 constexpr int kU = CMPC_ROWS_U;   // horizon unroll of the kernel (U in build_rows.hip)
 constexpr int kLdsBytes = 160 * 1024;
-constexpr int kWgPerCu = 3;       // resident workgroups per CU the kernel's VGPRs allow
 
 struct Pads {
   int order[CMPC_MAX_INPUTS];
@@ -223,6 +222,20 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
   return steps ? (double)extra / steps : 0.0;
 }
 
+// resident waves per CU of layout R with w waves per workgroup, at most 12
+// (3 waves/SIMD: the kernel's register budget)
+int waves_with(const RowsLayout& R, int w) {
+  // LDS is allocated in granules: count whole KiB (a layout 80 bytes over a
+  // third of the LDS measured as 2 resident workgroups, ser-cent p = 50)
+  const size_t lds = (sizeof(double) * ((size_t)R.lds_block + (size_t)R.per_wave * w) + 1023) / 1024 * 1024;
+  return lds <= (size_t)kLdsBytes ? std::min(12, (int)(kLdsBytes / lds) * w) : 0;
+}
+
+int resident_waves(const RowsLayout& R) {
+  const int w = cmpc_rows_waves_per_group(R);
+  return w ? waves_with(R, w) : 0;
+}
+
 uint64_t lcg(uint64_t& s) {
   s = s * 6364136223846793005ULL + 1442695040888963407ULL;
   return s >> 33;
@@ -230,6 +243,24 @@ uint64_t lcg(uint64_t& s) {
 
 
 }  // namespace
+
+// Workgroup size of the row kernel for layout R.  Four waves, unless two-wave
+// workgroups hold >= 1.5x the resident waves (a workgroup's waves go to
+// SIMDs in a fixed cyclic order, so small workgroups can pile onto a SIMD;
+// measured at p = 100: par-coop 6 vs 4 waves 0.72 vs 0.80 ms, ser-cent at
+// equal waves 0.68 vs 0.54 ms, one-wave workgroups slower still).  0 when
+// fewer than 4 waves per CU fit (one per SIMD): the one-QP-per-wave kernel
+// is faster there (cent p = 200: 1.36 vs 2.06 ms).  CMPC_ROWS_WPG=4|2
+// overrides it for timing.
+int cmpc_rows_waves_per_group(const RowsLayout& R) {
+  if (const char* e = std::getenv("CMPC_ROWS_WPG")) {
+    const int w = std::atoi(e);
+    if ((w == 4 || w == 2) && waves_with(R, w) > 0) return w;
+  }
+  const int w4 = waves_with(R, 4), w2 = waves_with(R, 2);
+  if (2 * w2 >= 3 * w4 && w2 >= 4) return 2;
+  return w4 >= 4 ? 4 : 0;
+}
 
 void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out) {
   std::memset(out, 0, sizeof *out);
@@ -249,17 +280,16 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
   Pads base{};
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
   RowsLayout best;
-  const size_t base_bytes = make_layout(d, nd, rec_len, base, &best);
+  make_layout(d, nd, rec_len, base, &best);
+  const int base_waves = resident_waves(best);
   // CMPC_ROWS_LAYOUT=packed: regions back to back (diagnostic A/B timing)
   const char* env = std::getenv("CMPC_ROWS_LAYOUT");
   const bool packed = env && std::strcmp(env, "packed") == 0;
   if (packed) {
-    best.ok = base_bytes <= (size_t)kLdsBytes;
-  } else if (base_bytes <= (size_t)kLdsBytes) {
-    // keep the workgroups per CU of the packed layout (at most kWgPerCu: the
-    // kernel's register budget, amdgpu_waves_per_eu(3) with 4 waves each)
-    const int wg = std::min(kWgPerCu, (int)(kLdsBytes / base_bytes));
-    const size_t budget = (size_t)(kLdsBytes / wg) / 512 * 512;
+    best.ok = base_waves > 0;
+  } else if (base_waves > 0) {
+    // keep the resident waves per CU of the packed layout (over the
+    // launcher's workgroup sizes, capped by the kernel's register budget)
     double best_cost = loop_conflicts(d, nd, best, 0);
     Pads bp = base;
     uint64_t seed = 0x5eedULL;
@@ -279,7 +309,8 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
         for (int i = d.nu_tot - 1; i > 0; --i) std::swap(cand.order[i], cand.order[lcg(seed) % (i + 1)]);
       }
       RowsLayout R;
-      if (make_layout(d, nd, rec_len, cand, &R) > budget) continue;
+      make_layout(d, nd, rec_len, cand, &R);
+      if (resident_waves(R) < base_waves) continue;
       const double cost = loop_conflicts(d, nd, R, 0);
       if (cost < best_cost) {
         best_cost = cost;
@@ -287,7 +318,8 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
         bp = cand;
       }
     }
-    best.ok = make_layout(d, nd, rec_len, bp, &best) <= (size_t)kLdsBytes;
+    make_layout(d, nd, rec_len, bp, &best);
+    best.ok = resident_waves(best) > 0;
   }
   std::lock_guard<std::mutex> lk(mu);
   cache[key] = best;
