@@ -145,9 +145,10 @@ void cmpc_build_rows_kernel(BuildParams P) {
     boff[k] = (k < ND) ? P.boff[k] : 0;
   }
   const int nseg = P.rows.nseg;
-  int segb[2 * CMPC_MAX_INPUTS];
+  constexpr int NSEG = 2 * NDW;  // segment bounds come from the delayed inputs (D, p - D)
+  int segb[NSEG];
 #pragma unroll
-  for (int i = 0; i < 2 * CMPC_MAX_INPUTS; ++i) segb[i] = P.rows.seg[i];
+  for (int i = 0; i < NSEG; ++i) segb[i] = P.rows.seg[i];
   double* const qlines = lines + R * LQ;  // this row's QP
   // readers (entry pointers; output o at +o, step u of a group at +u*NY)
   const bool rdel = gl && !zlane && dg > 0;
@@ -418,7 +419,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     for (int sg = 0; sg <= nseg; ++sg) {
       int r_end = pp;
 #pragma unroll
-      for (int i = 0; i < 2 * CMPC_MAX_INPUTS; ++i)
+      for (int i = 0; i < NSEG; ++i)
         if (i == sg && sg < nseg) r_end = segb[i];
       for (; r + U <= r_end; r += U) {
         CMPC_ROWS_STEP(0)
