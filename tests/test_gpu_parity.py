@@ -103,10 +103,12 @@ def test_gpu_build_matches_oracle(plant, ctype, p, variant):
 
 
 @pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "cent", 50),
-                                           ("ser", "coop", 100), ("par", "coop", 20)])
+                                           ("ser", "coop", 100), ("par", "coop", 20),
+                                           ("par", "coop", 100)])
 def test_gpu_build_variants_agree_large(plant, ctype, p):
     """Row-layout vs one-QP-per-wave build on a large batch (persistent grid,
-    several groups per wave): H, f, G agree to FP64 reassociation."""
+    several groups per wave): H, f, G agree to FP64 reassociation.  par-coop
+    p = 100 runs the row kernel in 2-wave workgroups."""
     _, setup, _, _ = setup_for(plant, ctype)
     cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
