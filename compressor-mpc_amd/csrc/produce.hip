@@ -149,19 +149,26 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   // records of the S sub-controllers of scenario b (per-QP mode: of slot q)
   const int s0 = P.per_qp ? unit - b * P.S : 0, s1 = P.per_qp ? s0 + 1 : P.S;
   const int dxs = P.per_qp ? P.dx_stride : P.naug;
+  // Record layout: [A B C f] from this scenario's LDS through the table,
+  // then the observer tail dx_aug (a straight copy: its loads do not wait on
+  // the table, and the loop has no branches), then y and the padding.
   for (int s = s0; s < s1; ++s) {
     const size_t q = (size_t)b * P.S + s;
     double* rec = P.lin + q * P.rec_len;
     const int* srow = src + s * P.rec_len;
-    for (int e = l; e < P.rec_len; e += kLanes) {
+    for (int e = l; e < P.off_x; e += kLanes) {
       const int t = srow[e];
-      double v;
-      if (t >= 0) v = w[t];
-      else if (t == kZero) v = 0.0;
-      else if (t == kOne) v = 1.0;
-      else if (t <= kDx) v = P.dx_aug ? P.dx_aug[q * dxs + (kDx - t)] : 0.0;
-      else v = P.y[(size_t)b * P.n_outputs + (kY - t)];
-      rec[e] = v;
+      rec[e] = (t >= 0) ? w[t] : (t == kOne ? 1.0 : 0.0);
+    }
+    if (P.dx_aug) {
+      const double* dx = P.dx_aug + q * dxs;
+      for (int e = l; e < P.naug; e += kLanes) rec[P.off_x + e] = dx[e];
+    } else {
+      for (int e = l; e < P.naug; e += kLanes) rec[P.off_x + e] = 0.0;
+    }
+    for (int e = P.off_x + P.naug + l; e < P.rec_len; e += kLanes) {
+      const int t = srow[e];  // y (kY - o) or padding (kZero)
+      rec[e] = (t == kZero) ? 0.0 : P.y[(size_t)b * P.n_outputs + (kY - t)];
     }
   }
 }
