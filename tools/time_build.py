@@ -17,6 +17,8 @@ for p in PS:
     cfg = cmpc.reference_config(PLANT, CTYPE, p=p)
     arr = cmpc.controller_arrays(cfg, reference_setup(PLANT, CTYPE))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
+    if os.environ.get("CMPC_TB_ZERO"):  # diagnostic: zero-filled records (power/clock test)
+        lin = np.zeros_like(lin); u = np.zeros_like(u)
     for v in VAR:
         with cmpc.Context(cfg, B) as ctx:
             ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
