@@ -482,7 +482,7 @@ struct HinvLds {
 // ---------------------------------------------------------------------------
 // Jacobi iterate kernel (lane per QP)
 // ---------------------------------------------------------------------------
-template <int N, int NU, int NVO>
+template <int N, int NU, int NVO, bool TRACE>
 __global__ __launch_bounds__(CMPC_SOLVE_THREADS)
 __attribute__((amdgpu_waves_per_eu(CMPC_SOLVE_WPE(N), CMPC_SOLVE_WPE(N))))
 void cmpc_solve_kernel(SolveParams P) {
@@ -544,7 +544,7 @@ void cmpc_solve_kernel(SolveParams P) {
   double x[N];
   QpOut o;
   if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
-    qp_solve<N, NU>(qp, pd, tol_d, f, 0u, CMPC_NWSR_MAX, x, o);
+    qp_solve_t<false>(qp, pd, tol_d, f, 0u, CMPC_NWSR_MAX, x, o);
     if (active) P.ws[q] = o.ws;
     return;
   }
@@ -584,11 +584,11 @@ void cmpc_solve_kernel(SolveParams P) {
         fk[a] = t;
       }
     }
-    qp_solve<N, NU>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
+    qp_solve_t<TRACE>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
     ws = o.ws;
 #pragma unroll
     for (int a = 0; a < N; ++a) dprev[a] = x[a];
-    if (active && P.trace) {
+    if (TRACE && active && P.trace) {
       uint32_t* tr = reinterpret_cast<uint32_t*>(P.trace + ((size_t)q * P.K + k) * 16);
 #pragma unroll
       for (int t = 0; t < 4; ++t) tr[t] = o.tr[t];
@@ -685,8 +685,12 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m, void*
 #define SOLVE_CASE(N_, NU_, NVO_)                                                      \
   if (nV == N_ && nu == NU_ && nVo == NVO_) {                                          \
     const int grid = (P.nqp + CMPC_SOLVE_THREADS - 1) / CMPC_SOLVE_THREADS;            \
-    hipLaunchKernelGGL((cmpc_solve_kernel<N_, NU_, NVO_>), dim3(grid),                 \
-                       dim3(CMPC_SOLVE_THREADS), 0, s, P);                             \
+    if (P.trace)                                                                       \
+      hipLaunchKernelGGL((cmpc_solve_kernel<N_, NU_, NVO_, true>), dim3(grid),         \
+                         dim3(CMPC_SOLVE_THREADS), 0, s, P);                           \
+    else                                                                               \
+      hipLaunchKernelGGL((cmpc_solve_kernel<N_, NU_, NVO_, false>), dim3(grid),        \
+                         dim3(CMPC_SOLVE_THREADS), 0, s, P);                           \
     return 0;                                                                          \
   }
 

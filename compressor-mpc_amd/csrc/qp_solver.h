@@ -272,8 +272,10 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
   return true;
 }
 
-template <int N, int NU, int NB, class HS>
-CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
+// TRACE = false: the working-set change trace (QpOut::tr, ntrace) is not
+// recorded (the iterate kernel without CMPC_TRACE); everything else is equal.
+template <bool TRACE, int N, int NU, int NB, class HS>
+CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
                          uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
   WSet<N> W;
   o.status = CMPC_QP_OK;
@@ -347,7 +349,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
         wj = W.j[a];
         wsd = W.side[a];
       }
-    trace_push(o, 0, wj, wsd);
+    if (TRACE) trace_push(o, 0, wj, wsd);
     wset_drop<N>(W, worst);
     if (++chg > max_chg) {
       o.status = CMPC_QP_MAX_NWSR;
@@ -443,7 +445,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
             kj = W.j[a];
             ks = W.side[a];
           }
-        trace_push(o, 0, kj, ks);
+        if (TRACE) trace_push(o, 0, kj, ks);
         wset_drop<N>(W, k);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
@@ -464,7 +466,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
         if (a < W.K) W.lam[a] = W.lam[a] - t * rv[a];
       up = up + t;
       if (full) {
-        trace_push(o, 1, pj, ps);
+        if (TRACE) trace_push(o, 1, pj, ps);
         wset_add<N>(W, pj, ps, up, np_, bp);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
@@ -481,7 +483,7 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
           kj = W.j[a];
           ks = W.side[a];
         }
-      trace_push(o, 0, kj, ks);
+      if (TRACE) trace_push(o, 0, kj, ks);
       wset_drop<N>(W, k);
       if (++chg > max_chg) {
         o.status = CMPC_QP_MAX_NWSR;
@@ -512,3 +514,9 @@ CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const d
   }
 }
 
+
+template <int N, int NU, int NB, class HS>
+CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
+                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
+  qp_solve_t<true>(q, pd, tol_d, g, ws_in, max_chg, x, o);
+}
