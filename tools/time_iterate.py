@@ -25,4 +25,6 @@ with cmpc.Context(cfg, B) as ctx:
     for _ in range(10): ctx.iterate(K)
     ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     _, _, ws_now = ctx.get_state()
-    print(f"iterate K={K}: {ms/n:.4f} ms  active fraction {(ws_now != 0).mean():.3f}", flush=True)
+    scen = (ws_now.reshape(B, cfg.S) != 0).any(axis=1).mean()
+    print(f"iterate K={K}: {ms/n:.4f} ms  active fraction {(ws_now != 0).mean():.3f} "
+          f"(scenarios {scen:.3f})", flush=True)
