@@ -286,6 +286,40 @@ def test_gpu_large_batch_properties():
                                atol=1e-10)
 
 
+def test_gpu_full_batch_kkt():
+    """At the bench size (coop-par p=50, B=65536, 131 072 QPs) every QP the
+    device solves is the QP optimum: a KKT certificate (feasibility, tight
+    active rows, multipliers >= 0, stationarity; relative 1e-9) from the
+    working set the kernel reports.  One Jacobi iteration from a random
+    neighbour plan, so g = f + G du_other is known on the host."""
+    from test_solver_kkt import kkt_certificate_batch, rows
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B, S, nu, m = 65536, cfg.S, cfg.nu, cfg.m
+    lin, u_old, _, ws = synthetic_batch(cfg, B, seed=1003, n_distinct=2048)
+    du_prev = np.random.default_rng(4).uniform(-0.05, 0.05, (B * S, cfg.nV))
+    with make_ctx(cfg, arr, B, lin, u_old, du_prev, ws) as ctx:
+        ctx.build()
+        ctx.init_warmstart()           # cold solves: sets the working sets only
+        H, f, G = ctx.download_qp()
+        ctx.iterate(1)
+        du, st, _ = ctx.download()
+        _, _, ws_out = ctx.get_state()
+    other = np.arange(B * S) ^ 1       # S = 2: the neighbour sub-controller
+    g = f + np.einsum("qij,qj->qi", G, du_prev[other])
+    s = np.arange(B * S) % S
+    uo = u_old[:, :nu]
+    lo = np.concatenate([np.tile(arr.lower[s] - uo, m), np.tile(arr.rate_lower[s], m)], axis=1)
+    hi = np.concatenate([np.tile(arr.upper[s] - uo, m), np.tile(arr.rate_upper[s], m)], axis=1)
+    okq = st == 0
+    assert okq.mean() > 0.999
+    cert = kkt_certificate_batch(H[okq], g[okq], lo[okq], hi[okq], rows(cfg.nV, nu), du[okq], ws_out[okq])
+    print("QPs solved:", okq.sum(), "with active constraints:", (ws_out[okq] != 0).mean())
+    assert cert.all(), np.flatnonzero(~cert)[:10]
+    assert (ws_out[okq] != 0).mean() > 0.05
+
+
 # SURVEY.md §8(d) configs restated as parity cases (the bench line is config
 # "coop p=50"; these run at their own sizes): (1) cent-ser at the reference's
 # p=100 (its CPU timing case, here batched B=4096), (2) coop-par p=20 B=4096

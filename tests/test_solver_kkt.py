@@ -67,6 +67,29 @@ def kkt_certificate(H, g, lo, hi, C, x, ws):
     assert np.abs(resid).max() <= 1e-9 * scale, ("stationarity", np.abs(resid).max(), scale)
 
 
+def kkt_certificate_batch(H, g, lo, hi, C, x, ws, tol=1e-9):
+    """kkt_certificate over a batch (Q QPs, rows C shared): boolean per QP.
+    Multipliers by batched pseudo-inverse of the signed active rows."""
+    Q, n = g.shape
+    bits = np.arange(C.shape[0], dtype=np.uint32)
+    ws = ws.astype(np.uint32)
+    act = ((ws[:, None] >> bits) & 1).astype(bool)
+    side = ((ws[:, None] >> (bits + 16)) & 1).astype(bool)
+    cx = x @ C.T
+    bscale = 1.0 + np.maximum(np.abs(lo), np.abs(hi))
+    ok = np.all((cx >= lo - tol * bscale) & (cx <= hi + tol * bscale), axis=1)
+    target = np.where(side, hi, lo)
+    ok &= np.all(~act | (np.abs(cx - target) <= tol * bscale), axis=1)
+    grad = np.einsum("qij,qj->qi", H, x) + g
+    N = C.T[None, :, :] * (np.where(side, -1.0, 1.0) * act)[:, None, :]
+    mu = np.einsum("qri,qi->qr", np.linalg.pinv(N), grad)
+    resid = grad - np.einsum("qir,qr->qi", N, mu)
+    scale = np.abs(H).max(axis=(1, 2)) * np.maximum(1.0, np.abs(x).max(axis=1)) + np.abs(g).max(axis=1) + 1.0
+    ok &= np.all(~act | (mu >= -tol * scale[:, None]), axis=1)
+    ok &= np.abs(resid).max(axis=1) <= tol * scale
+    return ok
+
+
 def enumerate_optimum(H, g, lo, hi, C):
     """The unique KKT point by enumeration (n <= 4)."""
     n = len(g)
@@ -151,6 +174,7 @@ def test_oracle_solver_kkt_condensed_qps(ctype):
     rng = np.random.default_rng(6)
     nu, m = cfg.nu, cfg.m
     ok = active = 0
+    batch = []
     for q in range(B * cfg.S):
         s = q % cfg.S
         H, f, _, _, G = O.build_qp(dims, lin[q], u_old[q], arr.y_ref[s], arr.ywt[s], arr.uwt[s])
@@ -163,6 +187,20 @@ def test_oracle_solver_kkt_condensed_qps(ctype):
         for ws_in in (0, random_ws(rng, len(g))):
             st = check(H, g, lb, ub, lbA, ubA, nu, ws_in, enumerate_n4=True)
             ok += st == OK
-            _, info = O.qp_solve(H, g, lb, ub, lbA, ubA, nu, ws_in)
+            x, info = O.qp_solve(H, g, lb, ub, lbA, ubA, nu, ws_in)
             active += st == OK and info.ws != 0
+            if st == OK:
+                batch.append((H, g, np.concatenate([lb, lbA]), np.concatenate([ub, ubA]), x, info.ws))
     assert ok >= 0.9 * 2 * B * cfg.S and active > 0, (ok, active)
+    # the batched certificate (used on the GPU's full-size output) agrees
+    H, g, lo, hi, x, ws = (np.array(a) for a in zip(*batch))
+    C = rows(len(g[0]), nu)
+    assert kkt_certificate_batch(H, g, lo, hi, C, x, ws).all()
+    # ... and rejects a perturbed solution and a wrong working set
+    x2 = x.copy()
+    x2[:, 0] += 1e-3 * (1.0 + np.abs(x).max(axis=1))
+    assert not kkt_certificate_batch(H, g, lo, hi, C, x2, ws).any()
+    flip = ws ^ np.uint32(1 << 16)  # flip the side bit of row 0
+    has0 = (ws & 1) == 1
+    if has0.any():
+        assert not kkt_certificate_batch(H, g, lo, hi, C, x, flip)[has0].any()
