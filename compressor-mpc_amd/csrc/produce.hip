@@ -33,8 +33,12 @@ constexpr int kWaves = 4;          // waves per workgroup
 constexpr int kSpw = 4;            // scenarios per wave: one per 16-lane row
 constexpr int kLanes = 64 / kSpw;  // lanes per scenario
 constexpr int kMat = 121;          // ns x ns, ns <= 11
-// per scenario: A, Ad, Bc, Bd, Cc, fc, fd, x, u
-constexpr int kScnLds = 2 * kMat + 4 * 44 + 2 * 11 + 2 * 11 + 3;
+// per scenario: A|Ad, Bc|Bd, Cc, fc|fd, x, u.  The discretised Ad, Bd, fd
+// overwrite A, Bc, fc: every lane holds its column of [A | B | f] in
+// registers before the first store, and one wave's LDS operations complete
+// in order.  (Separate arrays: 2 waves/SIMD by LDS, 0.140 ms at 65 536
+// scenarios; aliased, with the table sized by S: 4 waves/SIMD.)
+constexpr int kScnLds = kMat + 2 * 44 + 11 + 2 * 11 + 3;
 
 // Source of record element e of sub-controller s (same for every scenario):
 // >= 0: offset in the scenario's LDS region (Ad, Bd, Cc, fd); kZero, kOne;
@@ -44,7 +48,7 @@ constexpr int kZero = -1, kOne = -2, kDx = -1000, kY = -100;
 template <int PLANT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams P) {
   __shared__ double lds[kWaves * kSpw * kScnLds];
-  __shared__ int src[CMPC_MAX_S_PRODUCE * 2 * 64 * CMPC_REC_CHUNKS];
+  extern __shared__ int src[];  // S x rec_len (dynamic, cmpc_launch_produce)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane / kLanes, l = lane - g * kLanes;  // scenario row, lane in row
   // unit: scenario b (S records), or in per-QP mode QP slot q (its record)
@@ -55,9 +59,9 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   constexpr int ns = PLANT == CMPC_PLANT_PARALLEL ? 11 : 10;
   constexpr int ni = PLANT == CMPC_PLANT_PARALLEL ? 9 : 8;
   double* w = lds + (wave * kSpw + g) * kScnLds;
-  double *A = w, *Ad = A + kMat;
-  double *Bc = Ad + kMat, *Bd = Bc + 44, *Cc = Bd + 44, *fc = Cc + 44, *fd = fc + 11;
-  double *xs = fd + 11, *us = xs + 11;
+  double *A = w, *Ad = A;
+  double *Bc = A + kMat, *Bd = Bc, *Cc = Bc + 44, *fc = Cc + 44, *fd = fc;
+  double *xs = fc + 11, *us = xs + 11;
 
   // element -> source table (built once per workgroup)
   for (int t = threadIdx.x; t < P.S * P.rec_len; t += 64 * kWaves) {
@@ -179,12 +183,14 @@ int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int units = P.per_qp ? P.B * P.S : P.B;
   const int grid = (units + kWaves * kSpw - 1) / (kWaves * kSpw);
+  if (P.S < 1 || P.S > CMPC_MAX_S_PRODUCE || P.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return -1;
+  const size_t table = sizeof(int) * (size_t)P.S * P.rec_len;
   if (plant == CMPC_PLANT_PARALLEL)
-    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves), 0,
-                       s, P);
+    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves),
+                       table, s, P);
   else if (plant == CMPC_PLANT_SERIAL)
-    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_SERIAL>, dim3(grid), dim3(64 * kWaves), 0, s,
-                       P);
+    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_SERIAL>, dim3(grid), dim3(64 * kWaves),
+                       table, s, P);
   else
     return -1;
   return 0;
