@@ -153,44 +153,61 @@ struct Compressor {
   }
 };
 
+// Continuous linearisation of the parallel plant, split so that the device
+// producer runs the two compressors on two lanes: part(i) writes compressor
+// i's blocks and leaves its outlet flow and tank coupling in tk[2i], tk[2i+1];
+// tank() then adds the tank terms in the order of the single-lane loop.
+CMPC_PHD void parallel_linearize_part(int i, double p_in, const double* x, const double* u, double* A,
+                                      double* B, double* C, double* f, double* tk) {
+  const int ns = 11;
+  Compressor comp{CompressorParams(), true};
+  TankParams tank;
+  const double uc[6] = {u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3], p_in, x[10]};
+  double cA[25], cB[10], cC[10], cf[5], mo;
+  comp.linearize(x + 5 * i, uc, cA, cB, cC, cf, &mo);
+  for (int r = 0; r < 5; ++r) {
+    for (int k = 0; k < 5; ++k) A[(5 * i + r) * ns + 5 * i + k] = cA[r * 5 + k];
+    B[(5 * i + r) * 4 + 2 * i] = cB[r * 2];
+    B[(5 * i + r) * 4 + 2 * i + 1] = cB[r * 2 + 1];
+    f[5 * i + r] = cf[r];
+  }
+  for (int k = 0; k < 5; ++k) C[i * ns + 5 * i + k] = cC[5 + k];
+  tk[2 * i] = valve_flow(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, comp.P.m_out_c);
+  const double to_tank = valve_dpdp(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, tank.volume);
+  tk[2 * i + 1] = to_tank;
+  A[10 * ns + 5 * i + 1] = to_tank;
+  A[(5 * i + 1) * ns + 10] = valve_dpdp(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, comp.P.V2);
+  for (int k = 0; k < 5; ++k) C[2 * ns + 5 * i + k] = i ? -cC[k] : cC[k];
+}
+
+CMPC_PHD void parallel_linearize_tank(double p_out, const double* x, const double* u, double* A,
+                                      double* C, double* f, const double* tk) {
+  const int ns = 11;
+  TankParams tank;
+  double a = 0.0, flow_total = 0.0;
+  for (int i = 0; i < 2; ++i) {
+    flow_total += tk[2 * i];
+    a += -tk[2 * i + 1];
+  }
+  A[10 * ns + 10] = a + -valve_dpdp(x[10], p_out, u[8], tank.D, tank.volume);
+  C[3 * ns + 10] = 1;
+  f[10] = kC2 / tank.volume * (flow_total - valve_flow(x[10], p_out, u[8], tank.D, tank.m_out_c)) * 1e-5;
+}
+
 // Continuous linearisation of a reference plant: A ns x ns, B ns x 4, C 4 x ns, f ns.
 // zero_out = false: A, B, C are already zero (the device producer clears
 // them with the whole wave; one lane then writes only the nonzeros)
 CMPC_PHD void parallel_linearize(double p_in, double p_out, const double* x, const double* u, double* A,
                         double* B, double* C, double* f, bool zero_out = true) {
   const int ns = 11;
-  Compressor comp{CompressorParams(), true};
-  TankParams tank;
   if (zero_out) {
     zero(A, ns * ns);
     zero(B, ns * 4);
     zero(C, 4 * ns);
   }
-  double cC[2][10], flow_total = 0;
-  for (int i = 0; i < 2; ++i) {
-    const double uc[6] = {u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3], p_in, x[10]};
-    double cA[25], cB[10], cf[5], mo;
-    comp.linearize(x + 5 * i, uc, cA, cB, cC[i], cf, &mo);
-    for (int r = 0; r < 5; ++r) {
-      for (int k = 0; k < 5; ++k) A[(5 * i + r) * ns + 5 * i + k] = cA[r * 5 + k];
-      B[(5 * i + r) * 4 + 2 * i] = cB[r * 2];
-      B[(5 * i + r) * 4 + 2 * i + 1] = cB[r * 2 + 1];
-      f[5 * i + r] = cf[r];
-    }
-    for (int k = 0; k < 5; ++k) C[i * ns + 5 * i + k] = cC[i][5 + k];
-    flow_total += valve_flow(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, comp.P.m_out_c);
-    const double to_tank = valve_dpdp(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, tank.volume);
-    A[10 * ns + 5 * i + 1] = to_tank;
-    A[(5 * i + 1) * ns + 10] = valve_dpdp(x[5 * i + 1], x[10], u[4 * i + 2], comp.P.D, comp.P.V2);
-    A[10 * ns + 10] += -to_tank;
-  }
-  A[10 * ns + 10] += -valve_dpdp(x[10], p_out, u[8], tank.D, tank.volume);
-  for (int k = 0; k < 5; ++k) {
-    C[2 * ns + k] = cC[0][k];
-    C[2 * ns + 5 + k] = -cC[1][k];
-  }
-  C[3 * ns + 10] = 1;
-  f[10] = kC2 / tank.volume * (flow_total - valve_flow(x[10], p_out, u[8], tank.D, tank.m_out_c)) * 1e-5;
+  double tk[4];
+  for (int i = 0; i < 2; ++i) parallel_linearize_part(i, p_in, x, u, A, B, C, f, tk);
+  parallel_linearize_tank(p_out, x, u, A, C, f, tk);
 }
 
 // ParallelCompressors::GetDerivative (systems/parallel_compressors.cc:9-26;

@@ -38,7 +38,7 @@ constexpr int kMat = 121;          // ns x ns, ns <= 11
 // registers before the first store, and one wave's LDS operations complete
 // in order.  (Separate arrays: 2 waves/SIMD by LDS, 0.140 ms at 65 536
 // scenarios; aliased, with the table sized by S: 4 waves/SIMD.)
-constexpr int kScnLds = kMat + 2 * 44 + 11 + 2 * 11 + 3;
+constexpr int kScnLds = kMat + 2 * 44 + 11 + 2 * 11 + 3 + 4;
 
 // Source of record element e of sub-controller s (same for every scenario):
 // >= 0: offset in the scenario's LDS region (Ad, Bd, Cc, fd); kZero, kOne;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   double* w = lds + (wave * kSpw + g) * kScnLds;
   double *A = w, *Ad = A;
   double *Bc = A + kMat, *Bd = Bc, *Cc = Bc + 44, *fc = Cc + 44, *fd = fc;
-  double *xs = fc + 11, *us = xs + 11;
+  double *xs = fc + 11, *us = xs + 11, *tk = us + 14;  // tk: 4 (parallel plant)
 
   // element -> source table (built once per workgroup)
   for (int t = threadIdx.x; t < P.S * P.rec_len; t += 64 * kWaves) {
@@ -99,11 +99,16 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 #ifndef PRODUCE_EXP
 #define PRODUCE_EXP 0
 #endif
-  if (PRODUCE_EXP != 1 && valid && l == 0) {  // the scalar plant model, four scenarios side by side
-    if (PLANT == CMPC_PLANT_PARALLEL)
-      cmpc_plant::parallel_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc, false);
-    else
-      cmpc_plant::serial_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc, false);
+  // the scalar plant model, four scenarios side by side: the parallel
+  // plant's two compressors on lanes 0 and 1 of the row, then its tank
+  if (PLANT == CMPC_PLANT_PARALLEL) {
+    if (PRODUCE_EXP != 1 && valid && l < 2)
+      cmpc_plant::parallel_linearize_part(l, P.p_in, xs, us, A, Bc, Cc, fc, tk);
+    WAVE_SYNC();
+    if (PRODUCE_EXP != 1 && valid && l == 0)
+      cmpc_plant::parallel_linearize_tank(P.p_out, xs, us, A, Cc, fc, tk);
+  } else if (PRODUCE_EXP != 1 && valid && l == 0) {
+    cmpc_plant::serial_linearize(P.p_in, P.p_out, xs, us, A, Bc, Cc, fc, false);
   }
   WAVE_SYNC();
 
