@@ -98,13 +98,20 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_post_kernel(ObserverPara
   if (l < NO) yo[l] = yl;
 }
 
-// a priori + u_old update: one QP per wave (the delay blocks span ntot - nobs
-// entries, two per lane).  Looping several QPs per wave measured slower
-// (0.136 vs 0.111 ms for 131k QPs): the kernel is bound by load latency x
-// rounds of resident waves, so fewer waves in flight expose more of it.  Every source value is loaded before any store.
+// a priori + u_old update: CMPC_PRIOR_QPW QPs per wave side by side, one per
+// 64/QPW-lane group (the delay blocks span ntot - nobs = 80 entries, a few per
+// lane).  The kernel is bound by load latency x rounds of resident waves:
+// observe_apply for 131k QPs measured 0.113 ms at one QP per wave, 0.091 at
+// two, 0.085 at four; several QPs looped per wave were slower (0.136 ms).
+// Every source value is loaded before any store.
+#ifndef CMPC_PRIOR_QPW
+#define CMPC_PRIOR_QPW 4
+#endif
 template <int NS, int NUT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverParams P) {
-  const int lane = threadIdx.x & 63;
+  constexpr int kLq = 64 / CMPC_PRIOR_QPW;     // lanes per QP
+  constexpr int kH = (96 + kLq - 1) / kLq;     // aug entries per lane: kLq * kH >= ntot - nobs
+  const int lane = threadIdx.x & (kLq - 1), base = threadIdx.x & (64 - kLq);
   const int nobs = P.nobs, nd = P.nd;
   // delay tables in registers (compile-time indices: a runtime-indexed
   // kernel-argument read is a dependent memory load)
@@ -121,8 +128,9 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
     return v;
   };
-  const int q = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (q >= P.nqp) return;  // (whole waves exit together)
+  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * CMPC_PRIOR_QPW + base / kLq;
+  const bool valid = q_raw < P.nqp;  // (an idle half keeps the wave's shuffles)
+  const int q = valid ? q_raw : P.nqp - 1;
   double* st = P.obs + (size_t)q * P.obs_len;
   double* dx = st + NS;
   const double* rec = P.lin + (size_t)q * P.rec_len;
@@ -141,13 +149,13 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
 #pragma unroll
   for (int i = 0; i < NUT; ++i) brow[i] = rec[P.off_B + ls * NUT + i];
   const double fl = rec[P.off_f + ls];
-  // aug part, two entries per lane: slot k <- first state of block k; a block
-  // state <- its successor; the block's last state <- du' of its input (Baug)
-  double nv[2];
-  int tgt[2], from_du[2];
+  // aug part: slot k <- first state of block k; a block state <- its
+  // successor; the block's last state <- du' of its input (Baug)
+  double nv[kH];
+  int tgt[kH], from_du[kH];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int e = nobs + lane + 64 * h;
+  for (int h = 0; h < kH; ++h) {
+    const int e = nobs + lane + kLq * h;
     tgt[h] = -1;
     from_du[h] = -1;
     nv[h] = 0.0;
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
   const double seg = slot - useg;
   double dupv[NUT];
 #pragma unroll
-  for (int i = 0; i < NUT; ++i) dupv[i] = __shfl(dup, i, 64);
+  for (int i = 0; i < NUT; ++i) dupv[i] = __shfl(dup, base + i, 64);
   // states: (B du')[:ns] + (Adelay seg) + f
   double bsum = 0.0;
 #pragma unroll
@@ -180,7 +188,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
   double tsum = 0.0;
 #pragma unroll
   for (int k = 0; k < NUT; ++k) {
-    const double sk = __shfl(seg, k, 64);
+    const double sk = __shfl(seg, base + k, 64);
     double bk = brow[0];
 #pragma unroll
     for (int i = 1; i < NUT; ++i) bk = (din[k] == i) ? brow[i] : bk;
@@ -188,9 +196,10 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
   }
   const double xn = (bsum + tsum) + fl;
   WAVE_SYNC();  // all loads above have completed before the first store
+  if (!valid) return;
   if (lane < NS) dx[lane] = xn;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < kH; ++h) {
     if (tgt[h] < 0) continue;
     double val = nv[h];
 #pragma unroll
@@ -223,7 +232,8 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       return 0;
     }
     case CMPC_OBS_PRIOR: {
-      const int g8 = grid;  // one QP per wave
+      if (P.ntot - P.nobs > 96) return -1;  // the kernel's aug-entry budget
+      const int g8 = (P.nqp + CMPC_PRIOR_QPW * kWaves - 1) / (CMPC_PRIOR_QPW * kWaves);
       if (P.ns == 11 && P.nu_tot == 4)
         hipLaunchKernelGGL((cmpc_obs_prior_kernel<11, 4>), dim3(g8), dim3(64 * kWaves), 0, s, P);
       else if (P.ns == 10 && P.nu_tot == 4)
