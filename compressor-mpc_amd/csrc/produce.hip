@@ -161,19 +161,39 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   // Record layout: [A B C f] from this scenario's LDS through the table,
   // then the observer tail dx_aug (a straight copy: its loads do not wait on
   // the table, and the loop has no branches), then y and the padding.
+  // Each loop gathers kU values per lane into registers before storing them:
+  // the compiler cannot move a load of dx (or the table) above a store to
+  // rec it may alias, so a plain loop pays one load latency per element
+  // (cmpc_observe_step at 131 072 QP slots 0.220 -> 0.187 ms; scenario mode
+  // unchanged at 0.10 ms).
+  constexpr int kU = 8;
   for (int s = s0; s < s1; ++s) {
     const size_t q = (size_t)b * P.S + s;
     double* rec = P.lin + q * P.rec_len;
     const int* srow = src + s * P.rec_len;
-    for (int e = l; e < P.off_x; e += kLanes) {
-      const int t = srow[e];
-      rec[e] = (t >= 0) ? w[t] : (t == kOne ? 1.0 : 0.0);
+    for (int e0 = l; e0 < P.off_x; e0 += kU * kLanes) {
+      double v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + u * kLanes;
+        const int t = e < P.off_x ? srow[e] : kZero;
+        v[u] = (t >= 0) ? w[t] : (t == kOne ? 1.0 : 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (e0 + u * kLanes < P.off_x) rec[e0 + u * kLanes] = v[u];
     }
-    if (P.dx_aug) {
-      const double* dx = P.dx_aug + q * dxs;
-      for (int e = l; e < P.naug; e += kLanes) rec[P.off_x + e] = dx[e];
-    } else {
-      for (int e = l; e < P.naug; e += kLanes) rec[P.off_x + e] = 0.0;
+    const double* dx = P.dx_aug ? P.dx_aug + q * dxs : nullptr;
+    for (int e0 = l; e0 < P.naug; e0 += kU * kLanes) {
+      double v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + u * kLanes;
+        v[u] = (dx && e < P.naug) ? dx[e] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (e0 + u * kLanes < P.naug) rec[P.off_x + e0 + u * kLanes] = v[u];
     }
     for (int e = P.off_x + P.naug + l; e < P.rec_len; e += kLanes) {
       const int t = srow[e];  // y (kY - o) or padding (kZero)
