@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--input-batches", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend for the barrier and the max over ranks "
+                         "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -117,11 +120,16 @@ def main():
         log(f"note: WORLD_SIZE={world}, --gpus={args.gpus}; using WORLD_SIZE")
 
     import torch
+    if args.dist_backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     import cmpc
     from cmpc.configs import reference_setup
@@ -167,7 +175,8 @@ def main():
         dist.barrier()
     build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
@@ -231,6 +240,10 @@ def main():
             ctx.build()
             ctx.init_warmstart()
             ctx.synchronize()
+            # the isolated kernel timings below advance the observer and the
+            # plans without the build/iterate between them: snapshot the
+            # state and restore it before the full-step loop
+            obs_snap, state_snap = ctx.observer_state(), ctx.get_state()
             t0 = time.perf_counter()
             for _ in range(reps):
                 ctx.observe_step(tu.data_ptr(), ty.data_ptr())
@@ -241,6 +254,9 @@ def main():
                 ctx.observe_apply()
             ctx.synchronize()
             t_oa = (time.perf_counter() - t0) / reps
+            ctx.set_observer_state(obs_snap)
+            ctx.set_state(*state_snap)
+            ctx.synchronize()
             t0 = time.perf_counter()
             for _ in range(reps):
                 ctx.observe_step(tu.data_ptr(), ty.data_ptr())

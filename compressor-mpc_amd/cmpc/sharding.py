@@ -41,17 +41,20 @@ def shard_arrays(rank: int, world: int, S: int, *arrays):
 
 def gather_to_all(local: np.ndarray, n_total_qp: int, S: int, group=None) -> np.ndarray:
     """All-gather the per-rank per-QP results into the global scenario-major
-    array (works on gloo and nccl; with nccl the tensors must live on the
-    rank's GPU, which the caller arranges)."""
+    array.  On gloo the exchange runs on host tensors; on nccl (RCCL) the
+    padded shard and the receive buffers are placed on the rank's current GPU
+    and the result is copied back to the host."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     B = n_total_qp // S
     counts = [shard_range(B, world, r)[1] * S for r in range(world)]
     maxc = max(counts)
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend(group) == "nccl" else torch.device("cpu"))
     t = torch.from_numpy(np.ascontiguousarray(local))
-    pad = torch.zeros((maxc,) + tuple(t.shape[1:]), dtype=t.dtype)
-    pad[: t.shape[0]] = t
+    pad = torch.zeros((maxc,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    pad[: t.shape[0]] = t.to(dev)
     outs = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(outs, pad, group=group)
-    return np.concatenate([o[:c].numpy() for o, c in zip(outs, counts)], axis=0)
+    return np.concatenate([o[:c].cpu().numpy() for o, c in zip(outs, counts)], axis=0)

@@ -469,6 +469,10 @@ static int fill_produce(cmpc_ctx* c, const char* who, int plant, double p_in, do
   if (d.ns != ns || d.nu_tot != nci || d.ndist > no || d.ny > 4)
     return fail(std::string(who) + ": context dimensions do not match the plant");
   if (d.S > CMPC_MAX_S_PRODUCE) return fail(std::string(who) + ": too many sub-controllers");
+  if (L.rec_len > 2 * 64 * CMPC_REC_CHUNKS)
+    return fail(std::string(who) + ": lin record of " + std::to_string(L.rec_len) +
+                " doubles exceeds the producer's " + std::to_string(2 * 64 * CMPC_REC_CHUNKS) +
+                " (too many delay states)");
   std::memset(P, 0, sizeof *P);
   P->lin = c->lin;
   P->B = d.B;
@@ -574,6 +578,9 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
   if (c->obs_nout && c->obs_nout != n_outputs)
     return fail("cmpc_set_observer: n_outputs differs between sub-controllers");
   if (c->L.nobs > 32) return fail("cmpc_set_observer: ns + ndist > 32");
+  if (cmpc_obs_prior_shape(c->L.ntot - c->L.nobs, c->L.nd, d.nu_tot) <= 0)
+    return fail("cmpc_set_observer: " + std::to_string(c->L.ntot - c->L.nobs) +
+                " delay-block states per QP exceed the a-priori kernel's budget of 256 (sum of input delays)");
   for (int i = 0; i < d.nu_tot; ++i)
     if (d.delay[i] == 1) return fail("cmpc_set_observer: a one-step input delay has no delay block");
   HIP_TRY(hipSetDevice(c->device));
@@ -673,7 +680,8 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   ObserverParams P;
   observer_params(c, &P);
-  if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream)) return fail("observer launch failed");
+  if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream))
+    return fail("cmpc_observe_apply: no a-priori kernel instantiation for these dimensions");
   return check_launch("observer a-priori kernel");
 }
 

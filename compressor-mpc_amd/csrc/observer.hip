@@ -98,19 +98,19 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_post_kernel(ObserverPara
   if (l < NO) yo[l] = yl;
 }
 
-// a priori + u_old update: CMPC_PRIOR_QPW QPs per wave side by side, one per
-// 64/QPW-lane group (the delay blocks span ntot - nobs = 80 entries, a few per
-// lane).  The kernel is bound by load latency x rounds of resident waves:
-// observe_apply for 131k QPs measured 0.113 ms at one QP per wave, 0.091 at
-// two, 0.085 at four; several QPs looped per wave were slower (0.136 ms).
-// Every source value is loaded before any store.
-#ifndef CMPC_PRIOR_QPW
-#define CMPC_PRIOR_QPW 4
-#endif
-template <int NS, int NUT>
+// a priori + u_old update: QPW QPs per wave side by side, one per
+// 64/QPW-lane group (the delay blocks span ntot - nobs = 80 entries for the
+// reference plants, KH per lane).  The kernel is bound by load latency x
+// rounds of resident waves: observe_apply for 131k QPs measured 0.113 ms at
+// one QP per wave, 0.091 at two, 0.085 at four; several QPs looped per wave
+// were slower (0.136 ms).  The launcher picks the most QPs per wave whose
+// lanes hold every aug entry (cmpc_obs_prior_shape).  Every source value is
+// loaded before any store.
+template <int NS, int NUT, int QPW, int KH>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverParams P) {
-  constexpr int kLq = 64 / CMPC_PRIOR_QPW;     // lanes per QP
-  constexpr int kH = (96 + kLq - 1) / kLq;     // aug entries per lane: kLq * kH >= ntot - nobs
+  constexpr int kLq = 64 / QPW;  // lanes per QP
+  constexpr int kH = KH;         // aug entries per lane: kLq * kH >= ntot - nobs (launcher)
+  static_assert(kLq >= NS && kLq >= NUT, "a QP's lane group holds a state row per lane and every input");
   const int lane = threadIdx.x & (kLq - 1), base = threadIdx.x & (64 - kLq);
   const int nobs = P.nobs, nd = P.nd;
   // delay tables in registers (compile-time indices: a runtime-indexed
@@ -128,8 +128,8 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
     return v;
   };
-  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * CMPC_PRIOR_QPW + base / kLq;
-  const bool valid = q_raw < P.nqp;  // (an idle half keeps the wave's shuffles)
+  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * QPW + base / kLq;
+  const bool valid = q_raw < P.nqp;  // (an idle lane group keeps the wave's shuffles)
   const int q = valid ? q_raw : P.nqp - 1;
   double* st = P.obs + (size_t)q * P.obs_len;
   double* dx = st + NS;
@@ -213,6 +213,17 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
 
 }  // namespace
 
+// QPs per wave of the a-priori kernel for n_aug delay-block entries per QP
+// (lane group of 64/QPW lanes x the instantiation's entries per lane: 16 x 6,
+// 32 x 4, 64 x 4), 0 if none holds them.
+int cmpc_obs_prior_shape(int n_aug, int nd, int nu_tot) {
+  if (nd > 16 || nu_tot > 16) return 0;
+  if (n_aug <= 16 * 6) return 4;
+  if (n_aug <= 32 * 4) return 2;
+  if (n_aug <= 64 * 4) return 1;
+  return 0;
+}
+
 int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (P.nqp <= 0) return 0;
@@ -232,15 +243,20 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       return 0;
     }
     case CMPC_OBS_PRIOR: {
-      if (P.ntot - P.nobs > 96) return -1;  // the kernel's aug-entry budget
-      const int g8 = (P.nqp + CMPC_PRIOR_QPW * kWaves - 1) / (CMPC_PRIOR_QPW * kWaves);
-      if (P.ns == 11 && P.nu_tot == 4)
-        hipLaunchKernelGGL((cmpc_obs_prior_kernel<11, 4>), dim3(g8), dim3(64 * kWaves), 0, s, P);
-      else if (P.ns == 10 && P.nu_tot == 4)
-        hipLaunchKernelGGL((cmpc_obs_prior_kernel<10, 4>), dim3(g8), dim3(64 * kWaves), 0, s, P);
-      else
-        return -1;
-      return 0;
+      const int qpw = cmpc_obs_prior_shape(P.ntot - P.nobs, P.nd, P.nu_tot);
+      if (qpw <= 0) return -1;
+      const int g = (P.nqp + qpw * kWaves - 1) / (qpw * kWaves);
+#define OBS_PRIOR(NS_)                                                                        \
+  switch (qpw) {                                                                              \
+    case 4: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 4, 6>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
+    case 2: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 2, 4>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
+    case 1: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 1, 4>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
+  }
+      if (P.nu_tot != 4) return -1;
+      if (P.ns == 11) { OBS_PRIOR(11) }
+      if (P.ns == 10) { OBS_PRIOR(10) }
+#undef OBS_PRIOR
+      return -1;
     }
   }
   return -1;

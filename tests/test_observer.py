@@ -14,6 +14,8 @@ compare with.  Parity is therefore pinned three ways:
        all six reference step-0 goldens come out of the observer path
        (at t = 0 the a-posteriori update is the identity).
 """
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -77,8 +79,10 @@ def dense_post(ns, ndist, Cp, M, y, y_old, dx, x_hat):
     return dx, y.copy(), x_hat + dx[:ns]
 
 
-def setup(plant, ctype, p, B, seed, xs=0.005, us=0.01, ms=0.05):
+def setup(plant, ctype, p, B, seed, xs=0.005, us=0.01, ms=0.05, delays=None):
     cfg = cmpc.reference_config(plant, ctype, p=p)
+    if delays is not None:
+        cfg = dataclasses.replace(cfg, delays=tuple(delays))
     arr = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
     dims = CmpcDims.from_config(cfg, B)
     L = cmpc.layout_of(dims)
@@ -179,10 +183,15 @@ def lin_records(cfg, dims, L, xh, u_full, dx, y):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("plant,ctype", [("par", "coop"), ("ser", "cent")])
-def test_gpu_observer_kernels_match_oracle(plant, ctype):
-    B = 96
-    cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, 20, B, 5)
+@pytest.mark.parametrize("plant,ctype,B,delays", [
+    ("par", "coop", 96, None), ("ser", "cent", 96, None),
+    # B*S not a multiple of the 16 QPs per a-priori workgroup: the tail groups
+    ("par", "coop", 37, None), ("ser", "cent", 37, None),
+    # 120 and 140 delay-block states: the two- and one-QP-per-wave a-priori
+    # instantiations (the four-QP one holds 96)
+    ("par", "coop", 37, (0, 60, 0, 60)), ("par", "coop", 21, (0, 70, 0, 70))])
+def test_gpu_observer_kernels_match_oracle(plant, ctype, B, delays):
+    cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, 20, B, 5, delays=delays)
     nq = B * cfg.S
     dx0 = rng.normal(0, 1e-3, (nq, L.ntot))
     with cmpc.Context(cfg, B, device=0) as ctx:
