@@ -3,8 +3,8 @@
 # Every GPU step has its own time limit; a crash/timeout ends the script.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
-TAG=${1:-r1}
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/test_$TAG.log 2>&1
+TAG=${1:-r2}
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/test_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
