@@ -57,6 +57,9 @@
 #ifndef CMPC_ROWS_PF
 #define CMPC_ROWS_PF 0  // L2 prefetch of the next group's records (2% slower with LDS staging)
 #endif
+#ifndef CMPC_ROWS_FUSE
+#define CMPC_ROWS_FUSE 1  // chain and gather FMAs of a step in one interleaved block
+#endif
 #ifndef CMPC_ROWS_PRIO
 #define CMPC_ROWS_PRIO 1  // 1: priority by progress; 2: + prologue at top priority
 #endif
@@ -378,17 +381,30 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // offsets).  The LDS reads of a step are consumed one step later (yh at the
 // chain start, rd after the chain), and the scheduling barrier keeps the
 // compiler from sinking them next to their use.
+#if CMPC_ROWS_FUSE && CMPC_RX != 3
+// the running sum of the gather columns first (rd was read a step earlier),
+// then the chain and the gather FMAs in one interleaved block: 4 + nV
+// accumulators in flight (same FMA order per accumulator as two blocks)
+#define CMPC_ROWS_CG()                                                      \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o)                          \
+        cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
+    rows_chain_gacc<NS, NY, ND, NUT, NU, M>(pP, pS, mP, mS, aP, aS, cv, acc); \
+    __builtin_amdgcn_sched_barrier(0);
+#else
+#define CMPC_ROWS_CG()                                                      \
+    rows_chain<NS, NY, ND>(pP, pS, mP, mS, aP, aS);                         \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o)                          \
+        cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
+    if (CMPC_RX != 3) rows_gacc<NY, NUT, NU, M>(cv, acc);
+#endif
 #define CMPC_ROWS_STEP(u)                                                   \
   {                                                                         \
     double aS = base + yh;                                                  \
     yh = yp[u];                                                             \
     double aP[NY];                                                          \
     _Pragma("unroll") for (int o = 0; o < NY; ++o) aP[o] = 0.0;             \
-    rows_chain<NS, NY, ND>(pP, pS, mP, mS, aP, aS);                         \
-    __builtin_amdgcn_sched_barrier(0);                                      \
-    _Pragma("unroll") for (int o = 0; o < NY; ++o)                          \
-        cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
-    if (CMPC_RX != 3) rows_gacc<NY, NUT, NU, M>(cv, acc);                   \
+    CMPC_ROWS_CG()                                                          \
     _Pragma("unroll") for (int o = 0; o < NY; ++o) pP[o] = aP[o];           \
     pS = aS;                                                                \
     if (CMPC_RX != 1 && CMPC_RX != 4) {                                     \
@@ -446,6 +462,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     }
 #undef CMPC_ROWS_STEP
 #undef CMPC_ROWS_TAIL
+#undef CMPC_ROWS_CG
 #pragma unroll
     for (int o = 0; o < NY; ++o) cv[o] = __builtin_fma(smask, cv[o], rd[o]);
     rows_gacc<NY, NUT, NU, M>(cv, acc);  // row p - 1

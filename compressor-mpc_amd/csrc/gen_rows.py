@@ -25,6 +25,9 @@ CTRL = "row_mask:0xf bank_mask:0xf"
 # used by the instantiated kernels (build_rows.hip launcher list)
 CHAINS = [(11, 3, 2), (11, 2, 2), (10, 2, 2), (10, 4, 2)]
 GACCS = [(3, 4, 2, 2), (2, 4, 2, 2), (3, 4, 4, 2), (4, 4, 2, 2), (4, 4, 4, 2), (3, 4, 2, 1)]
+# (NS, NY, ND, NUT, NU, M) of the fused chain + gather blocks (the launcher's cases)
+FUSED = [(11, 3, 2, 4, 2, 2), (11, 2, 2, 4, 2, 2), (11, 3, 2, 4, 4, 2), (10, 2, 2, 4, 2, 2),
+         (10, 4, 2, 4, 2, 2), (10, 4, 2, 4, 4, 2), (11, 3, 2, 4, 2, 1)]
 
 
 def chain(ns, ny, nd):
@@ -66,6 +69,45 @@ def gacc(ny, nut, nu, mm):
             f"  asm({body}\n      : {outs}\n      : {ins});\n}}\n")
 
 
+def chain_gacc(ns, ny, nd, nut, nu, mm):
+    """rows_chain and rows_gacc of one step in one block: the gather FMAs are
+    spread between the chain's link groups, so 4 + nV accumulators are in
+    flight instead of 4 (microbench_hybrid V3: -4 % per step at 3 waves/SIMD).
+    Same FMA order per accumulator as the two separate blocks."""
+    nv = nu * mm
+    o_aS = ny
+    o_acc = [ny + 1 + a for a in range(nv)]
+    i0 = ny + 1 + nv
+    o_pP = [i0 + o for o in range(ny)]
+    o_pS = i0 + ny
+    o_mP = [o_pS + 1 + l for l in range(ns)]
+    o_mS = [o_pS + 1 + ns + l for l in range(ns + nd)]
+    o_cv = [o_pS + 1 + ns + ns + nd + o for o in range(ny)]
+    gl = []
+    for o in range(ny):
+        for a in range(nv):
+            src = (a // nu) * nut + a % nu
+            gl.append(f'"v_fmac_f64_dpp %{o_acc[a]}, %{o_cv[o]}, %{o_cv[o]} row_newbcast:{src} {CTRL}\\n\\t"')
+    per = -(-len(gl) // ns)  # gather FMAs after each link group
+    lines = ['"s_nop 1\\n\\t"']
+    for l in range(ns):
+        for o in range(ny):
+            lines.append(f'"v_fmac_f64_dpp %{o}, %{o_pP[o]}, %{o_mP[l]} row_newbcast:{l} {CTRL}\\n\\t"')
+        lines.append(f'"v_fmac_f64_dpp %{o_aS}, %{o_pS}, %{o_mS[l]} row_newbcast:{l} {CTRL}\\n\\t"')
+        lines.extend(gl[l * per:(l + 1) * per])
+    for k in range(nd):
+        lines.append(f'"v_fmac_f64_dpp %{o_aS}, %{o_pS}, %{o_mS[ns + k]} row_newbcast:{16 - nd + k} {CTRL}\\n\\t"')
+    outs = ", ".join([f'"+v"(aP[{o}])' for o in range(ny)] + ['"+v"(aS)'] + [f'"+v"(acc[{a}])' for a in range(nv)])
+    ins = ", ".join([f'"v"(pP[{o}])' for o in range(ny)] + ['"v"(pS)'] +
+                    [f'"v"(mP[{l}])' for l in range(ns)] + [f'"v"(mS[{l}])' for l in range(ns + nd)] +
+                    [f'"v"(cv[{o}])' for o in range(ny)])
+    body = "\n      ".join(lines)
+    return (f"template <> __device__ __forceinline__ void rows_chain_gacc<{ns}, {ny}, {nd}, {nut}, {nu}, {mm}>("
+            f"const double* pP, double pS, const double* mP, const double* mS, double* aP, double& aS, "
+            f"const double* cv, double* acc) {{\n"
+            f"  asm({body}\n      : {outs}\n      : {ins});\n}}\n")
+
+
 def main():
     parts = ["// Generated by gen_rows.py — do not edit.\n",
              "template <int NS, int NY, int ND> __device__ __forceinline__ void rows_chain("
@@ -76,6 +118,11 @@ def main():
         parts.append(chain(*c))
     for g in GACCS:
         parts.append(gacc(*g))
+    parts.append("template <int NS, int NY, int ND, int NUT, int NU, int M> __device__ __forceinline__ void "
+                 "rows_chain_gacc(const double*, double, const double*, const double*, double*, double&, "
+                 "const double*, double*);\n")
+    for c in FUSED:
+        parts.append(chain_gacc(*c))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)

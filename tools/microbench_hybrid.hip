@@ -75,6 +75,34 @@ __device__ __forceinline__ void chain33(double* aP, double& aS, const double* pP
                  "v"(n[9]), "v"(n[10]), "v"(n[11]), "v"(n[12]));
 }
 
+
+// V3: the 46 chain links and the 12 gather FMAs of a step interleaved in one
+// block (8 independent accumulators instead of 4, then 4)
+__device__ __forceinline__ void chain_gather(double* aP, double& aS, const double* pP, double pS, const double* m,
+                                             const double* n, double* acc, const double* cv) {
+  asm volatile("s_nop 1\n\t"
+#define C(l, r, s)                                                   \
+  "v_fmac_f64_dpp %0, %8, %" #r " row_newbcast:" #l " " CTRL "\n\t" \
+  "v_fmac_f64_dpp %1, %9, %" #r " row_newbcast:" #l " " CTRL "\n\t" \
+  "v_fmac_f64_dpp %2, %10, %" #r " row_newbcast:" #l " " CTRL "\n\t" \
+  "v_fmac_f64_dpp %3, %11, %" #s " row_newbcast:" #l " " CTRL "\n\t"
+#define G(a, o, l) "v_fmac_f64_dpp %" #a ", %" #o ", %" #o " row_newbcast:" #l " " CTRL "\n\t"
+               C(0, 12, 23) G(4, 36, 0) G(5, 36, 1) C(1, 13, 24) G(6, 36, 4) G(7, 36, 5) C(2, 14, 25)
+               G(4, 37, 0) G(5, 37, 1) C(3, 15, 26) G(6, 37, 4) G(7, 37, 5) C(4, 16, 27) G(4, 38, 0)
+               G(5, 38, 1) C(5, 17, 28) G(6, 38, 4) G(7, 38, 5) C(6, 18, 29) C(7, 19, 30) C(8, 20, 31)
+               C(9, 21, 32) C(10, 22, 33)
+#undef C
+#undef G
+               "v_fmac_f64_dpp %3, %11, %34 row_newbcast:14 " CTRL "\n\t"
+               "v_fmac_f64_dpp %3, %11, %35 row_newbcast:15 " CTRL "\n\t"
+               : "+v"(aP[0]), "+v"(aP[1]), "+v"(aP[2]), "+v"(aS), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]),
+                 "+v"(acc[3])
+               : "v"(pP[0]), "v"(pP[1]), "v"(pP[2]), "v"(pS), "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]),
+                 "v"(m[4]), "v"(m[5]), "v"(m[6]), "v"(m[7]), "v"(m[8]), "v"(m[9]), "v"(m[10]), "v"(n[0]),
+                 "v"(n[1]), "v"(n[2]), "v"(n[3]), "v"(n[4]), "v"(n[5]), "v"(n[6]), "v"(n[7]), "v"(n[8]),
+                 "v"(n[9]), "v"(n[10]), "v"(n[11]), "v"(n[12]), "v"(cv[0]), "v"(cv[1]), "v"(cv[2]));
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void kern(const double* __restrict__ in, double* out, long long* clk) {
   const int lane = threadIdx.x & 63;
@@ -83,7 +111,7 @@ __global__ __launch_bounds__(256) void kern(const double* __restrict__ in, doubl
   for (int g = 0; g < NGRP; ++g) {
     const double* src = in + ((blockIdx.x * 4 + (threadIdx.x >> 6)) * NGRP + g) % 4096 * 64 * 64;
     auto ld = [&](int i) { return src[i * 64 + lane]; };
-    if constexpr (V == 0) {
+    if constexpr (V == 0 || V == 3) {
       double pP[3], pS, m[11], n[13], acc[4] = {0, 0, 0, 0}, cv[3] = {0, 0, 0};
       for (int i = 0; i < 3; ++i) pP[i] = ld(i);
       pS = ld(3);
@@ -94,11 +122,18 @@ __global__ __launch_bounds__(256) void kern(const double* __restrict__ in, doubl
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           double aP[3] = {0.0, 0.0, 0.0}, aS = rd0;
-          chain33(aP, aS, pP, pS, m, n);
-          cv[0] = __builtin_fma(sm, cv[0], rd0);
-          cv[1] = __builtin_fma(sm, cv[1], rd1);
-          cv[2] = __builtin_fma(sm, cv[2], rd2);
-          gather(acc, cv);
+          if constexpr (V == 0) {
+            chain33(aP, aS, pP, pS, m, n);
+            cv[0] = __builtin_fma(sm, cv[0], rd0);
+            cv[1] = __builtin_fma(sm, cv[1], rd1);
+            cv[2] = __builtin_fma(sm, cv[2], rd2);
+            gather(acc, cv);
+          } else {
+            chain_gather(aP, aS, pP, pS, m, n, acc, cv);
+            cv[0] = __builtin_fma(sm, cv[0], rd0);
+            cv[1] = __builtin_fma(sm, cv[1], rd1);
+            cv[2] = __builtin_fma(sm, cv[2], rd2);
+          }
           pP[0] = aP[0]; pP[1] = aP[1]; pP[2] = aP[2]; pS = aS;
         }
       }
@@ -208,6 +243,7 @@ int main() {
   (void)hipMemcpy(in, h.data(), sizeof(double) * nin, hipMemcpyHostToDevice);
   for (int w : {2, 3, 4}) {
     timeit<0>("V0 dpp", w, in, out, clk);
+    timeit<3>("V3 dpp ilp", w, in, out, clk);
     timeit<1>("V1 hybrid", w, in, out, clk);
     timeit<2>("V2 mfma", w, in, out, clk);
   }
