@@ -83,8 +83,16 @@ def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
     reps = max(1, int(round(target_s / max(t_pass, 1e-6))))
     dt = run(nb, threads, reps)
     t_single = run(probe, 1, 1)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {
         "value": nb * S * K / dt,
+        "cpu_model": model,
+        "host_cpus": os.cpu_count(),
         "seconds": dt * reps,
         "unit": "QP solves/s",
         "cores": threads,
@@ -183,6 +191,26 @@ def main():
 
     du, st, nw = ctx.download()
     _, _, ws_now = ctx.get_state()
+
+    # K = 1 (the build-dominated figure beside the K = 9 headline),
+    # this rank, after the headline measurement
+    k1 = None
+    try:
+        for i in range(2):
+            ctx.bind_lin(batches[i % NB].data_ptr())
+            ctx.step(1, 0)
+        ctx.synchronize()
+        reps1 = max(10, args.steps // 2)
+        t0 = time.perf_counter()
+        for i in range(reps1):
+            ctx.bind_lin(batches[i % NB].data_ptr())
+            ctx.step(1, 0)
+        ctx.synchronize()
+        t_k1 = (time.perf_counter() - t0) / reps1
+        k1 = {"qp_solves_per_s_per_gpu": B * S / t_k1, "ms_per_step": t_k1 * 1e3, "steps": reps1,
+              "note": "K = 1 Jacobi iteration per step (build-dominated), this rank's GPU"}
+    except Exception as e:  # reported, never required
+        log(f"K=1 variant failed: {e}")
 
     # Closed-loop variant (reported beside the metric, not in `value`): the
     # records are produced on the device from plant states each step
@@ -338,6 +366,7 @@ def main():
         },
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1)},
+        "k1": k1,
         "qp_status_ok_fraction": ok_frac,
         "qp_active_constraint_fraction": active_frac,
         "mean_working_set_changes_last_solve": mean_chg,
