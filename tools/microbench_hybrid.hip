@@ -210,7 +210,9 @@ void timeit(const char* name, int wps, const double* in, double* out, long long*
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  for (int rep = 0; rep < 30; ++rep) hipLaunchKernelGGL(kern<V>, dim3(grid), dim3(256), 0, 0, in, out, clk);
+  // settle: ~0.3 s of launches (the clock ramps over the first ~40 ms of load)
+  for (int rep = 0; rep < 300 * 4 / wps; ++rep)
+    hipLaunchKernelGGL(kern<V>, dim3(grid), dim3(256), 0, 0, in, out, clk);
   const int R = 10;
   (void)hipEventRecord(e0);
   for (int rep = 0; rep < R; ++rep) hipLaunchKernelGGL(kern<V>, dim3(grid), dim3(256), 0, 0, in, out, clk);
