@@ -54,6 +54,17 @@
 #ifndef CMPC_RX
 #define CMPC_RX 0
 #endif
+// Timing-only prologue/epilogue ablations (results invalid; tools/build_variant.sh):
+// 1: no record staging (the region keeps the previous group's tables),
+// 2: staging without the wait (the compiler still waits before the first LDS
+//    read: only the explicit wait goes), 3: no QP stores.  At the steady
+//    clock, 1 is 9-11 % faster; the same bytes through plain vector loads
+//    instead of LDS-DMA are as slow as the product, and issuing the DMA
+//    without any wait (asm-issued, round 2) too: the cost is the HBM read
+//    itself, not its latency or the DMA issue.
+#ifndef CMPC_PX
+#define CMPC_PX 0
+#endif
 #ifndef CMPC_ROWS_PF
 #define CMPC_ROWS_PF 0  // L2 prefetch of the next group's records (2% slower with LDS staging)
 #endif
@@ -217,7 +228,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     // tables below overwrite once the records are read.  (Reading the records
     // with per-lane global loads took ~15 dependent round trips per group, and
     // L2 evicted records in between: 2.5x the algorithmic HBM bytes.)
-    {
+    if (CMPC_PX != 1) {
       const int nq = min(4, nqp - 4 * g);
       const int nchunk = nq * rec_len / 2;
       const double* gsrc = P.lin + (size_t)4 * g * rec_len;
@@ -232,7 +243,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
 #pragma unroll
     for (int k = 0; k < NDW; ++k) uo[k] = (k < ND) ? P.u_old[(size_t)qq * NUT + dinp[k]] : 0.0;
     CMPC_T(0)  // staging issue
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (CMPC_PX != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CMPC_T(1)  // staging wait
     const double* srec = wreg + R * rec_len;  // this row's record (staged)
     const double* xa = srec + P.off_x;
@@ -469,7 +480,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     asm volatile("" ::"v"(pf0), "v"(pf1));
     CMPC_T(3)  // horizon loop
 
-    if (qv && gl && !CMPC_ROWS_TIMING) {
+    if (qv && gl && !CMPC_ROWS_TIMING && CMPC_PX != 3) {
       double* out = P.qp + (size_t)q * P.qp_len;
       constexpr int nuo = NUT - NU, nVo = M * nuo;
       const double* uwt = uw_all + s * NU * NU;
