@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--K", type=int, default=9)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-seconds", type=float, default=0.25)
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,6 +61,11 @@ def main():
     for _ in range(args.warmup):
         cr.step(K)
     torch.cuda.synchronize()
+    # settle: the clock ramps over the first ~40 ms of load (tools/time_clock_ramp.py)
+    t_end = time.perf_counter() + args.settle_seconds
+    while time.perf_counter() < t_end:
+        cr.step(K)
+        torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

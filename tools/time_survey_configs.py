@@ -4,6 +4,7 @@ Config 4 (64 sub-controllers over 8 GPUs) is tools/bench_coupled.py.
 usage: python tools/time_survey_configs.py"""
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
@@ -31,10 +32,13 @@ for name, plant, ctype, p, B, K in CONFIGS:
         ctx.upload_lin(lin)
         ctx.build()
         ctx.init_warmstart()
-        for _ in range(3):
-            ctx.build()
-            ctx.iterate(K)
-        ctx.synchronize()
+        # settle: the clock ramps over the first ~40 ms of load (tools/time_clock_ramp.py)
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
+            for _ in range(4):
+                ctx.build()
+                ctx.iterate(K)
+            ctx.synchronize()
         ctx.enable_timing(True)
         for _ in range(REPS):
             ctx.build()
