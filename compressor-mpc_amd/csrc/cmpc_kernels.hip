@@ -1,3 +1,6 @@
+#ifndef CMPC_SOLVE_CACHE
+#define CMPC_SOLVE_CACHE 1  // reuse the working-set factors across Jacobi iterations
+#endif
 #include <algorithm>
 // MI355X (gfx950) kernels of the condensed-QP hot path.
 //
@@ -551,6 +554,12 @@ void cmpc_solve_kernel(SolveParams P) {
   double dprev[N];
 #pragma unroll
   for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+#if CMPC_SOLVE_CACHE
+  // working set + factors of the previous Jacobi iteration's solve (same H):
+  // reused when the working set is unchanged (qp_solve_t, CACHE)
+  WSet<N> wc;
+  uint32_t wc_ws = kWsInvalid;
+#endif
   for (int k = 0; k < P.K; ++k) {
 #if CMPC_SOLVE_PRIO
     {  // fair progress of the SIMD's waves (cf. build_rows.hip)
@@ -584,7 +593,11 @@ void cmpc_solve_kernel(SolveParams P) {
         fk[a] = t;
       }
     }
+#if CMPC_SOLVE_CACHE
+    qp_solve_t<TRACE, true>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o, &wc, &wc_ws);
+#else
     qp_solve_t<TRACE>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
+#endif
     ws = o.ws;
 #pragma unroll
     for (int a = 0; a < N; ++a) dprev[a] = x[a];

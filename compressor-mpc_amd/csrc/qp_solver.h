@@ -274,20 +274,37 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
 
 // TRACE = false: the working-set change trace (QpOut::tr, ntrace) is not
 // recorded (the iterate kernel without CMPC_TRACE); everything else is equal.
-template <bool TRACE, int N, int NU, int NB, class HS>
+//
+// CACHE = true (the Jacobi loop of the iterate kernel): the caller keeps the
+// working set of the previous solve of the same QP (same H, other g) in *wc,
+// with *wc_ws its working-set word, or kWsInvalid.  When ws_in equals it, the
+// warm start takes the slots and the LDL' factors of M = N' H^-1 N from *wc
+// instead of rebuilding them: the same values (a deterministic function of H
+// and the working set), so the result and the trace are bit-identical to the
+// uncached solve.  *wc_ws is set only after a solve that ends OK with its
+// factors matching its slots.
+constexpr uint32_t kWsInvalid = 0xFFFFFFFFu;
+
+template <bool TRACE, bool CACHE = false, int N, int NU, int NB, class HS>
 CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
-                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
-  WSet<N> W;
+                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o,
+                         WSet<N>* wc = nullptr, uint32_t* wc_ws = nullptr) {
+  WSet<N> Wl;
+  WSet<N>& W = CACHE ? *wc : Wl;
+  const bool cached = CACHE && pd && *wc_ws == ws_in;
+  bool fact_ok = cached;  // W.L, W.D are the factors of the current slots
   o.status = CMPC_QP_OK;
   o.nchg = 0;
   o.ntrace = 0;
   o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
-  W.K = 0;
+  if (!cached) {
+    W.K = 0;
 #pragma unroll
-  for (int a = 0; a < N; ++a) {
-    W.j[a] = 0;
-    W.side[a] = 0;
-    W.lam[a] = 0.0;
+    for (int a = 0; a < N; ++a) {
+      W.j[a] = 0;
+      W.side[a] = 0;
+      W.lam[a] = 0.0;
+    }
   }
   int chg = 0;
   bool done = false;
@@ -305,7 +322,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   }
   // A. warm start: slot a = the a-th active constraint of ws_in in ascending
   // j (the oracle adds them in that order while K < n)
-  {
+  if (!cached) {
     uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
 #pragma unroll
     for (int a = 0; a < N; ++a) {
@@ -323,10 +340,13 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     }
   }
   for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
-    if (!wset_factor<N>(q, W)) {
-      W.K = 0;
-      ++chg;
-      continue;
+    if (!(fact_ok && it == 0)) {
+      fact_ok = wset_factor<N>(q, W);
+      if (!fact_ok) {
+        W.K = 0;
+        ++chg;
+        continue;
+      }
     }
     double rhs[N];
 #pragma unroll
@@ -351,6 +371,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       }
     if (TRACE) trace_push(o, 0, wj, wsd);
     wset_drop<N>(W, worst);
+    fact_ok = false;
     if (++chg > max_chg) {
       o.status = CMPC_QP_MAX_NWSR;
       done = true;
@@ -452,7 +473,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
           done = true;
           break;
         }
-        wset_factor<N>(q, W);
+        fact_ok = wset_factor<N>(q, W);
         continue;
       }
       const double sl = ndot<N>(np_, x) - bp;
@@ -473,7 +494,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
           done = true;
           break;
         }
-        wset_factor<N>(q, W);
+        fact_ok = wset_factor<N>(q, W);
         break;
       }
       int kj = 0, ks = 0;
@@ -490,7 +511,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         done = true;
         break;
       }
-      wset_factor<N>(q, W);
+      fact_ok = wset_factor<N>(q, W);
     }
   }
   o.nchg = chg;
@@ -499,6 +520,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   for (int a = 0; a < N; ++a)
     if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
   o.ws = w;
+  if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && fact_ok) ? w : kWsInvalid;
   if (o.status == CMPC_QP_OK) {
     // variables at an active bound are fixed exactly at it
 #pragma unroll

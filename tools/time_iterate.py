@@ -19,10 +19,13 @@ if os.environ.get("CMPC_TI_UNCONSTRAINED"):  # diagnostic: bounds far away, no a
 with cmpc.Context(cfg, B) as ctx:
     ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
     ctx.build(); ctx.init_warmstart()
-    for _ in range(3): ctx.iterate(K)
-    ctx.synchronize()
+    import time
+    t_end = time.perf_counter() + float(os.environ.get("CMPC_TB_SETTLE", "0.3"))  # clock settle
+    while time.perf_counter() < t_end:
+        for _ in range(8): ctx.iterate(K)
+        ctx.synchronize()
     ctx.enable_timing(True)
-    for _ in range(10): ctx.iterate(K)
+    for _ in range(40): ctx.iterate(K)
     ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     _, _, ws_now = ctx.get_state()
     scen = (ws_now.reshape(B, cfg.S) != 0).any(axis=1).mean()
