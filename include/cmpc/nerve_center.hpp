@@ -163,10 +163,20 @@ struct SetupFile {
   }
 };
 
+// ControllerInterface<System> (include/controller_interface.h:18-50): the
+// pure-virtual interface every reference controller implements.  A harness
+// that holds its controller as ControllerInterface* keeps doing so.
+class ControllerInterface {
+ public:
+  virtual ~ControllerInterface() = default;
+  /// const ControlInput GetNextInput(const Output& y) (controller_interface.h:46)
+  virtual std::vector<double> GetNextInput(const double* y) = 0;
+};
+
 // NerveCenter<System, n_total_states, SubControllers...> for one plant
 // (B = 1, as the reference); `handle()` exposes the context for the batched
 // entry points of include/cmpc.h.
-class NerveCenter {
+class NerveCenter : public ControllerInterface {
  public:
   NerveCenter(const ControllerSpec& spec, int n_solver_iterations, int device = 0)
       : spec_(spec), K_(n_solver_iterations) {
@@ -301,7 +311,9 @@ class NerveCenter {
 
   /// ControllerInterface::GetNextInput(y) (controller_interface.h:46), the
   /// observer on the device (SetObserver).
-  std::vector<double> GetNextInput(const double* y) { return GetNextInputWithTiming(y, -1, nullptr); }
+  std::vector<double> GetNextInput(const double* y) override {
+    return GetNextInputWithTiming(y, -1, nullptr);
+  }
 
   /// NerveCenter::GetNextInputWithTiming(y, n_timing_iterations, time_out)
   /// (nerve_center.h:134-182), the observer on the device.

@@ -5,7 +5,7 @@
 // GetNextInputWithTiming.  Prints the applied control input u(t = 0) with 6
 // significant digits (the precision of the reference's results/*.dat).
 //
-// usage: nerve_center_step0 <setup-file> <par|ser> <cent|coop|ncoop> [p] [observer]
+// usage: nerve_center_step0 <setup-file> <par|ser> <cent|coop|ncoop> [p] [observer|iface]
 // "observer": SetObserver for every sub-controller (an arbitrary gain: the
 // t = 0 correction is zero) and the reference's GetNextInputWithTiming(y, n, t).
 #include <cstdio>
@@ -29,7 +29,10 @@ int main(int argc, char** argv) {
     const ControllerSpec spec = ControllerSpec::Reference(plant, type, p);
     const SetupFile setup = SetupFile::Read(argv[1]);
 
-    const bool observer = argc > 5 && std::strcmp(argv[5], "observer") == 0;
+    // "iface": as "observer", called through the ControllerInterface base
+    // (controller_interface.h:46), the way a harness holding any controller does
+    const bool iface = argc > 5 && std::strcmp(argv[5], "iface") == 0;
+    const bool observer = iface || (argc > 5 && std::strcmp(argv[5], "observer") == 0);
     NerveCenter nc(spec, setup.n_iterations);
     if (observer) {
       const int nobs = spec.ns + spec.ndist;
@@ -68,10 +71,12 @@ int main(int argc, char** argv) {
     nc.Initialize(x0.data(), u0.data(), u_full.data(), y0.data());
     int64_t ns_time = 0;
     // t = 0: the observer's a-posteriori correction is zero, x_hat = x0
+    cmpc::ControllerInterface& ctrl = nc;
     const std::vector<double> u =
-        observer ? nc.GetNextInputWithTiming(y0.data(), setup.n_timing_iterations, &ns_time)
-                 : nc.GetNextInputWithTiming(y0.data(), x0.data(), nullptr,
-                                             setup.n_timing_iterations, &ns_time);
+        iface ? ctrl.GetNextInput(y0.data())
+        : observer ? nc.GetNextInputWithTiming(y0.data(), setup.n_timing_iterations, &ns_time)
+                   : nc.GetNextInputWithTiming(y0.data(), x0.data(), nullptr,
+                                               setup.n_timing_iterations, &ns_time);
     for (int c = 0; c < spec.nu_tot; ++c) std::printf("%s%.6g", c ? " " : "", u[c]);
     std::printf("\n");
     std::fprintf(stderr, "status:");

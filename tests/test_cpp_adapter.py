@@ -77,17 +77,20 @@ def test_setup_writer_roundtrip(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("observer", [False, True], ids=["external-estimate", "device-observer"])
+@pytest.mark.parametrize("observer", [False, True, "iface"],
+                         ids=["external-estimate", "device-observer", "controller-interface"])
 @pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser"])
 def test_gpu_cpp_adapter_step0_matches_reference(name, observer, tmp_path):
     """The reference's call pattern through cmpc::NerveCenter; with
-    SetObserver the reference's own GetNextInputWithTiming(y, n, t)."""
+    SetObserver the reference's own GetNextInputWithTiming(y, n, t), or
+    GetNextInput(y) through the ControllerInterface base."""
     _build()
     cfg, _, _, g = GC.case(name)
     ctype, plant = name.split("-")
     setup = tmp_path / f"setup-{name}"
     write_setup(setup, g, cfg.ny, cfg.S)
-    args = [DRIVER, str(setup), plant, ctype, "100"] + (["observer"] if observer else [])
+    mode = {False: [], True: ["observer"], "iface": ["iface"]}[observer]
+    args = [DRIVER, str(setup), plant, ctype, "100"] + mode
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     u = [float(t) for t in r.stdout.split()]
