@@ -539,7 +539,7 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
     per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   const int need = std::max(1, ((P.nqp + 3) / 4 + WPG - 1) / WPG);
   const int grid = std::max(1, std::min(need, P.cus * per_cu));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPG), lds, s, P);
+  cmpc_launch(kern, dim3(grid), dim3(64 * WPG), lds, s, P);
   return 0;
 }
 

@@ -64,6 +64,8 @@ int layout_of(const cmpc_dims* d, cmpc_layout* L) {
 
 }  // namespace
 
+thread_local LaunchEvents cmpc_launch_events;
+
 struct cmpc_ctx {
   cmpc_dims d{};
   cmpc_layout L{};
@@ -176,19 +178,25 @@ hipError_t pooled_event(cmpc_ctx* c, hipEvent_t* e) {
   return hipEventCreate(e);
 }
 
+// A timed launch: the launcher (cmpc_launch, cmpc_internal.h) passes both
+// events to hipExtLaunchKernelGGL, which writes the kernel's start and end
+// into them; no marker packets go into the stream.
 int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
   (void)k;
+  cmpc_launch_events = LaunchEvents{};
   if (!c->timing) return 0;
+  hipEvent_t e1;
   HIP_TRY(pooled_event(c, e0));
-  HIP_TRY(hipEventRecord(*e0, c->stream));
+  HIP_TRY(pooled_event(c, &e1));
+  cmpc_launch_events.start = *e0;
+  cmpc_launch_events.stop = e1;
   return 0;
 }
 
 int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
+  const hipEvent_t e1 = cmpc_launch_events.stop;
+  cmpc_launch_events = LaunchEvents{};
   if (!c->timing) return 0;
-  hipEvent_t e1;
-  HIP_TRY(pooled_event(c, &e1));
-  HIP_TRY(hipEventRecord(e1, c->stream));
   c->pending[k].push_back({e0, e1});
   c->launches[k]++;
   return 0;
@@ -1161,6 +1169,7 @@ int cmpc_init_warmstart(cmpc_ctx* c) {
   SolveParams P;
   solve_params(c, &P);
   P.init = 1;
+  cmpc_launch_events = LaunchEvents{};  // untimed (a failed timed launch may have left them set)
   if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
     return fail("solve kernel not instantiated for these dimensions");
   return check_launch("init kernel");

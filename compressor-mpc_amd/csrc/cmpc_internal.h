@@ -1,9 +1,27 @@
 // Internal launch parameters shared by cmpc_abi.cpp (host) and
 // cmpc_kernels.hip (device).  Not part of the public ABI.
 #pragma once
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/cmpc.h"
+
+// Kernel timing (cmpc_enable_timing).  cmpc_abi.cpp sets these events around
+// a timed launch (null otherwise); the launchers hand them to
+// hipExtLaunchKernelGGL, which stamps the kernel's own start and end into
+// them from its dispatch packet.  hipEventRecord markers before and after
+// each kernel cost ~7 us per bench step (tools/time_step_gaps.py).  One
+// context per host thread (cmpc.h), hence thread_local.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchEvents cmpc_launch_events;
+template <typename F, typename... A>
+inline void cmpc_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t stream, A... args) {
+  hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, stream, cmpc_launch_events.start,
+                        cmpc_launch_events.stop, 0u, args...);
+}
 
 #define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
 #define CMPC_BUILD_WAVES 4       // waves per build workgroup (one QP per wave at a time)

@@ -677,8 +677,8 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
             lds) != hipSuccess || per_cu < 1)                                         \
       per_cu = std::max<int>(1, (int)((160 * 1024) / lds));                            \
     const int grid = std::max(1, std::min(P.grid, P.cus * per_cu));                   \
-    hipLaunchKernelGGL((cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>), dim3(grid),           \
-                       dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                        \
+    cmpc_launch((cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>), dim3(grid),                  \
+                dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                               \
     return 0;                                                                          \
   }
 
@@ -699,11 +699,11 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m, void*
   if (nV == N_ && nu == NU_ && nVo == NVO_) {                                          \
     const int grid = (P.nqp + CMPC_SOLVE_THREADS - 1) / CMPC_SOLVE_THREADS;            \
     if (P.trace)                                                                       \
-      hipLaunchKernelGGL((cmpc_solve_kernel<N_, NU_, NVO_, true>), dim3(grid),         \
-                         dim3(CMPC_SOLVE_THREADS), 0, s, P);                           \
+      cmpc_launch((cmpc_solve_kernel<N_, NU_, NVO_, true>), dim3(grid),                \
+                  dim3(CMPC_SOLVE_THREADS), 0, s, P);                                  \
     else                                                                               \
-      hipLaunchKernelGGL((cmpc_solve_kernel<N_, NU_, NVO_, false>), dim3(grid),        \
-                         dim3(CMPC_SOLVE_THREADS), 0, s, P);                           \
+      cmpc_launch((cmpc_solve_kernel<N_, NU_, NVO_, false>), dim3(grid),               \
+                  dim3(CMPC_SOLVE_THREADS), 0, s, P);                                  \
     return 0;                                                                          \
   }
 

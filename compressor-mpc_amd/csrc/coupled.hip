@@ -104,7 +104,7 @@ int cmpc_launch_coupled(const CoupledParams& P, int n, int nu, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int grid = (P.nqp + 255) / 256;
   if (n == 4 && nu == 2) {
-    hipLaunchKernelGGL((cmpc_coupled_kernel<4, 2>), dim3(grid), dim3(256), 0, s, P);
+    cmpc_launch((cmpc_coupled_kernel<4, 2>), dim3(grid), dim3(256), 0, s, P);
     return 0;
   }
   return -1;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU parity suite, the step-gap tool, and a bench line without the CPU leg.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" && mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tq.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/tq.log; tail -3 gpurun_out/tq.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python tools/time_step_gaps.py 2>&1 | grep -v amdgpu.ids || exit $?
+for i in 1 2; do
+timeout -k 10 300 python bench.py --no-cpu > gpurun_out/bq.json 2> gpurun_out/bq.err || exit $?
+python3 -c "import json; d=json.loads(open('gpurun_out/bq.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['kernels_ms_per_step'])"
+done
