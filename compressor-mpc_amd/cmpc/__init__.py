@@ -292,8 +292,15 @@ class Context:
         check(self.lib.cmpc_download_trace(self._h, bptr(trace), iptr(ntrace)), "download_trace")
         return trace, ntrace
 
-    def enable_timing(self, on: bool = True):
-        check(self.lib.cmpc_enable_timing(self._h, int(on)), "enable_timing")
+    def enable_timing(self, on: bool = True, only=None):
+        """Kernel timing: every kernel (on), none, or only the kernel ids in
+        `only` (CMPC_KERNEL_BUILD / CMPC_KERNEL_ITERATE)."""
+        flag = int(bool(on))
+        if on and only is not None:
+            flag = 0
+            for k in only:
+                flag |= 2 << k
+        check(self.lib.cmpc_enable_timing(self._h, flag), "enable_timing")
 
     def kernel_time(self, kernel: int):
         ms = ctypes.c_double()

@@ -103,7 +103,7 @@ struct cmpc_ctx {
   int build_variant = CMPC_BUILD_AUTO;
   int last_build = 0;  // kernel launched by the last cmpc_build
   // timing
-  bool timing = false;
+  int timing = 0;  // bit k: kernel k is timed
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
   std::vector<hipEvent_t> event_pool;  // reused so timing stays cheap in a timed loop
   double tot_ms[2] = {0, 0};
@@ -182,9 +182,8 @@ hipError_t pooled_event(cmpc_ctx* c, hipEvent_t* e) {
 // events to hipExtLaunchKernelGGL, which writes the kernel's start and end
 // into them; no marker packets go into the stream.
 int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
-  (void)k;
   cmpc_launch_events = LaunchEvents{};
-  if (!c->timing) return 0;
+  if (!((c->timing >> k) & 1)) return 0;
   hipEvent_t e1;
   HIP_TRY(pooled_event(c, e0));
   HIP_TRY(pooled_event(c, &e1));
@@ -196,7 +195,7 @@ int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
 int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
   const hipEvent_t e1 = cmpc_launch_events.stop;
   cmpc_launch_events = LaunchEvents{};
-  if (!c->timing) return 0;
+  if (!((c->timing >> k) & 1)) return 0;
   c->pending[k].push_back({e0, e1});
   c->launches[k]++;
   return 0;
@@ -1302,7 +1301,7 @@ int cmpc_download_trace(cmpc_ctx* c, uint8_t* trace, int32_t* ntrace) {
 int cmpc_enable_timing(cmpc_ctx* c, int enable) {
   if (!c) return fail("null context");
   if (resolve_timing(c)) return -1;
-  c->timing = enable != 0;
+  c->timing = enable == 0 ? 0 : enable == 1 ? 3 : (enable >> 1) & 3;
   for (int k = 0; k < 2; ++k) {
     c->tot_ms[k] = 0;
     c->launches[k] = 0;

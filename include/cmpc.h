@@ -179,9 +179,12 @@ int cmpc_download_qp(cmpc_ctx* ctx, double* H, double* f, double* G);
  * 0xFF terminates), ntrace: B*S*K counts. */
 int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
 
-/* Per-kernel device time (HIP events on the ctx stream, opt-in). */
+/* Per-kernel device time (HIP events stamped by the kernel's own dispatch,
+ * opt-in).  enable: 0 off, 1 every kernel, or an OR of CMPC_TIME_ONLY(k)
+ * to time only those kernels (the others launch without events). */
 #define CMPC_KERNEL_BUILD 0
 #define CMPC_KERNEL_ITERATE 1
+#define CMPC_TIME_ONLY(kernel) (2 << (kernel))
 int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
 int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,
                      int64_t* launches);

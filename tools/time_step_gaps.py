@@ -25,17 +25,23 @@ with cmpc.Context(cfg, B) as ctx:
     for _ in range(10):
         ctx.step(K, 0)
     ctx.synchronize()
-    for timing in (False, True, False, True):
-        ctx.enable_timing(timing)
+    for timing in (False, True, "build", False, True, "build"):
+        if timing == "build":
+            ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+        else:
+            ctx.enable_timing(timing)
         t0 = time.perf_counter()
         for _ in range(STEPS):
             ctx.step(K, 0)
         ctx.synchronize()
         dt = (time.perf_counter() - t0) / STEPS * 1e3
-        line = f"timing events {'on ' if timing else 'off'}: {dt:.4f} ms per step"
-        if timing:
+        line = f"timing events {'off' if not timing else 'on ' if timing is True else timing}: {dt:.4f} ms per step"
+        if timing is True:
             bms, nb = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
             ims, ni = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
             ks = bms / nb + ims / ni
             line += f"  kernels {ks:.4f} ms (build {bms / nb:.4f}, iterate {ims / ni:.4f}), gap {dt - ks:.4f} ms"
+        if timing == "build":
+            bms, nb = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+            line += f"  build {bms / nb:.4f} ms"
         print(line, flush=True)
