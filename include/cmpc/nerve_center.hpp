@@ -7,6 +7,7 @@
 // Reference interface mirrored (paths relative to the reference root):
 //   ControllerInterface<System>::GetNextInput(y)      include/controller_interface.h:46
 //   NerveCenter ctor (controllers, n_solver_iterations) include/nerve_center.h:89-95
+//   DistributedController(sys, constraints, M)         include/distributed_controller.h:126-128
 //   NerveCenter::Initialize(x, u, u_full, y, dx)      include/nerve_center.h:98-104
 //   NerveCenter::SetWeights(uwt, ywt)                 include/nerve_center.h:107-110
 //   NerveCenter::SetWeights(uwt, {ywt_s})             include/nerve_center.h:113-116
@@ -163,6 +164,32 @@ struct SetupFile {
   }
 };
 
+// InputConstraints<nu> (include/input_constraints.h:12-26): bounds on one
+// sub-controller's own inputs, nu values each.  As in the reference the rate
+// rows are always part of the QP and use_rate_constraints is never read
+// (SURVEY.md 8, quirk 9).
+struct InputConstraints {
+  std::vector<double> lower_bound, upper_bound, lower_rate_bound, upper_rate_bound;
+  bool use_rate_constraints = false;
+};
+
+// DistributedController<AugLinSys, ...>(sys, constraints, M)
+// (include/distributed_controller.h:126-128): the constructor arguments of
+// one sub-controller.  Its template arguments (plant, index maps, delays,
+// p, m) are the ControllerSpec; M is the (ns + ndist) x n_outputs observer
+// gain, row-major (empty: no device observer, see NerveCenter).
+class DistributedController {
+ public:
+  explicit DistributedController(InputConstraints constraints, std::vector<double> M = {})
+      : constraints_(std::move(constraints)), M_(std::move(M)) {}
+  const InputConstraints& constraints() const { return constraints_; }
+  const std::vector<double>& observer_matrix() const { return M_; }
+
+ private:
+  InputConstraints constraints_;
+  std::vector<double> M_;
+};
+
 // ControllerInterface<System> (include/controller_interface.h:18-50): the
 // pure-virtual interface every reference controller implements.  A harness
 // that holds its controller as ControllerInterface* keeps doing so.
@@ -202,6 +229,29 @@ class NerveCenter : public ControllerInterface {
     u_old_.assign(spec.nu_tot, 0.0);
     u_offset_.assign(spec.n_inputs, 0.0);
     rec_.assign(static_cast<size_t>(spec.S()) * L_.rec_len, 0.0);
+  }
+  /// NerveCenter(controllers, n_solver_iterations) (nerve_center.h:89-95):
+  /// from the sub-controllers, in sub-controller order, as the reference
+  /// harness builds NvCtr from its DistributedController tuple.
+  NerveCenter(const ControllerSpec& spec, const std::vector<DistributedController>& controllers,
+              int n_solver_iterations, int device = 0)
+      : NerveCenter(spec, n_solver_iterations, device) {
+    if (static_cast<int>(controllers.size()) != spec.S())
+      throw Error("NerveCenter: " + std::to_string(controllers.size()) + " sub-controllers for a " +
+                  std::to_string(spec.S()) + "-controller spec");
+    for (int s = 0; s < spec.S(); ++s) {
+      const InputConstraints& c = controllers[s].constraints();
+      for (const auto* v : {&c.lower_bound, &c.upper_bound, &c.lower_rate_bound, &c.upper_rate_bound})
+        if (static_cast<int>(v->size()) != spec.nu) throw Error("InputConstraints: nu values per bound");
+      SetConstraints(s, c.lower_bound.data(), c.upper_bound.data(), c.lower_rate_bound.data(),
+                     c.upper_rate_bound.data());
+      if (!controllers[s].observer_matrix().empty()) {
+        if (static_cast<int>(controllers[s].observer_matrix().size()) !=
+            (spec.ns + spec.ndist) * spec.n_outputs)
+          throw Error("DistributedController: M must be (ns + ndist) x n_outputs");
+        SetObserver(s, controllers[s].observer_matrix().data());
+      }
+    }
   }
   ~NerveCenter() {
     if (ctx_) cmpc_destroy(ctx_);

@@ -33,13 +33,31 @@ int main(int argc, char** argv) {
     // (controller_interface.h:46), the way a harness holding any controller does
     const bool iface = argc > 5 && std::strcmp(argv[5], "iface") == 0;
     const bool observer = iface || (argc > 5 && std::strcmp(argv[5], "observer") == 0);
-    NerveCenter nc(spec, setup.n_iterations);
-    if (observer) {
-      const int nobs = spec.ns + spec.ndist;
-      std::vector<double> M(static_cast<size_t>(nobs) * spec.n_outputs, 0.0);
-      for (int o = 0; o < spec.ndist && o < spec.n_outputs; ++o) M[(spec.ns + o) * spec.n_outputs + o] = 0.5;
-      for (int s = 0; s < spec.S(); ++s) nc.SetObserver(s, M.data());
+    // the sub-controllers (InputConstraints, observer gain M), then the
+    // NerveCenter over them, as the reference harness builds NvCtr
+    std::vector<DistributedController> subs;
+    for (int s = 0; s < spec.S(); ++s) {
+      // nu values, or nu_tot in plant control-input order
+      auto sub = [&](const std::vector<double>& v) {
+        std::vector<double> r(spec.nu);
+        for (int c = 0; c < spec.nu; ++c)
+          r[c] = static_cast<int>(v.size()) == spec.nu ? v[c] : v[spec.input_order[s][c]];
+        return r;
+      };
+      InputConstraints ic;
+      ic.lower_bound = sub(setup.lower);
+      ic.upper_bound = sub(setup.upper);
+      ic.lower_rate_bound = sub(setup.rate_lower);
+      ic.upper_rate_bound = sub(setup.rate_upper);
+      std::vector<double> M;
+      if (observer) {  // an arbitrary gain: the t = 0 correction is zero
+        const int nobs = spec.ns + spec.ndist;
+        M.assign(static_cast<size_t>(nobs) * spec.n_outputs, 0.0);
+        for (int o = 0; o < spec.ndist && o < spec.n_outputs; ++o) M[(spec.ns + o) * spec.n_outputs + o] = 0.5;
+      }
+      subs.emplace_back(ic, M);
     }
+    NerveCenter nc(spec, subs, setup.n_iterations);
     // weights: uwt is n_control_inputs^2; ywt one ny x ny block per sub-controller
     const int blk = spec.ny * spec.ny;
     std::vector<const double*> ywt(spec.S());
@@ -51,18 +69,6 @@ int main(int argc, char** argv) {
     for (int i = 0; i < spec.p; ++i)
       for (int o = 0; o < spec.n_outputs; ++o) y_ref[i * spec.n_outputs + o] = setup.yref[o];
     nc.SetOutputReference(y_ref.data());
-    // InputConstraints of each sub-controller (nu values, or nu_tot in plant order)
-    for (int s = 0; s < spec.S(); ++s) {
-      auto sub = [&](const std::vector<double>& v) {
-        std::vector<double> r(spec.nu);
-        for (int c = 0; c < spec.nu; ++c)
-          r[c] = static_cast<int>(v.size()) == spec.nu ? v[c] : v[spec.input_order[s][c]];
-        return r;
-      };
-      const auto lo = sub(setup.lower), up = sub(setup.upper);
-      const auto rlo = sub(setup.rate_lower), rup = sub(setup.rate_upper);
-      nc.SetConstraints(s, lo.data(), up.data(), rlo.data(), rup.data());
-    }
     // operating point: the plant's default state and input (u_offset)
     std::vector<double> x0(spec.ns), u_full(spec.n_inputs), y0(spec.n_outputs);
     Check(cmpc_plant_default(static_cast<int>(plant), x0.data(), u_full.data()), "cmpc_plant_default");
