@@ -90,8 +90,11 @@
 #define CMPC_T(i)
 #endif
 
+#ifndef CMPC_ROWS_WPE
+#define CMPC_ROWS_WPE 3  // waves per SIMD the kernel is compiled and launched for
+#endif
 template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG>
-__global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(CMPC_ROWS_WPE, CMPC_ROWS_WPE)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -537,6 +540,7 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPG, lds) != hipSuccess ||
       per_cu < 1)
     per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
+  per_cu = std::min(per_cu, std::max(1, 4 * CMPC_ROWS_WPE / WPG));  // ablation: fewer waves per SIMD
   const int need = std::max(1, ((P.nqp + 3) / 4 + WPG - 1) / WPG);
   const int grid = std::max(1, std::min(need, P.cus * per_cu));
   cmpc_launch(kern, dim3(grid), dim3(64 * WPG), lds, s, P);
