@@ -161,6 +161,12 @@ void cmpc_build_rows_kernel(BuildParams P) {
     dlen[k] = (k < ND) ? P.dlen[k] : 0;
     boff[k] = (k < ND) ? P.boff[k] : 0;
   }
+  // a carrier's w line is zero from t = D on: at the loop segment r = D its
+  // reads move to the zero slots, so the w table holds D + 3 entries, not p + 6
+  int ysw = -1;
+#pragma unroll
+  for (int k = 0; k < NDW; ++k)
+    if (cl && k == kc && dlen[k] < pp) ysw = dlen[k];
   const int nseg = P.rows.nseg;
   constexpr int NSEG = 2 * NDW;  // segment bounds come from the delayed inputs (D, p - D)
   int segb[NSEG];
@@ -473,6 +479,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
       }
       if (r == rsw) { rq = r_line; rinc = NY; }
       if (r == wsw) { wq = dump; winc = 0; }
+      if (r == ysw) { yp = zeros; yinc = 0; }
     }
 #undef CMPC_ROWS_STEP
 #undef CMPC_ROWS_TAIL

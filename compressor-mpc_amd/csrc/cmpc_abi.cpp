@@ -1145,9 +1145,12 @@ int cmpc_build(cmpc_ctx* c) {
   int rc = -1;
   // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
   // than the one-QP-per-wave kernel for every plant/controller type at
-  // p = 20, 50, 100: tools/gpu_config_sweep.sh), else the
-  // one-QP-per-wave kernel (e.g. cent p = 200)
-  if (c->build_variant == CMPC_BUILD_ROWS || c->build_variant == CMPC_BUILD_AUTO)
+  // p = 20, 50, 100, 200: tools/gpu_config_sweep.sh, tools/gpu_long_horizon.sh,
+  // DESIGN.md §3.0) and the batch gives it at least one wave per SIMD; else
+  // the one-QP-per-wave kernel, which has four times the waves for a small
+  // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
+  const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
+  if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_fill))
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)
     return fail("row-layout build kernel not available for these dimensions");

@@ -65,7 +65,11 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
   R->LQ = up(o, 2) + 2 * pd.LQ;
   R->ch_off = 4 * R->LQ;
   R->w_off = R->ch_off + 4 * ny * 16 + pd.w;
-  R->WL = up(d.p + 2 + U, 2) + pd.WL;
+  // w lines: the carriers read entries 3 + r (r < p) until the segment r = D
+  // of their input, then the zero slots (build_rows.hip): D + 3 entries
+  int dmax = 0;
+  for (int c = 0; c < d.nu_tot; ++c) dmax = std::max(dmax, d.delay[c]);
+  R->WL = up(std::min(d.p + 2 + U, dmax + 3), 2) + pd.WL;
   // the group's four records are staged over the wave's region first
   R->per_wave = std::max(up(R->w_off + 4 * nd * R->WL, 2), up(4 * rec_len, 2));
   R->yls = d.p + U + pd.yls;
@@ -113,7 +117,10 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
   const int NG = M * NUT + 1;
   const int wreg = R.lds_block + wave * R.per_wave;
   int rq[64], rinc[64], rline[64], rsw[64], wq[64], winc[64], wsw[64], dump[64], yp[64], yinc[64];
-  int zq[64], tq[64];
+  int zq[64], tq[64], ysw[64];
+  int kdelay[CMPC_ND_MAX] = {0};  // delay of the k-th delayed input (ascending input index)
+  for (int c = 0, k = 0; c < d.nu_tot && k < CMPC_ND_MAX; ++c)
+    if (d.delay[c] > 0) kdelay[k++] = d.delay[c];
   bool mk[64], ol[64], tl[64], all[64];
   for (int lane = 0; lane < 64; ++lane) {
     const int Rw = lane >> 4, j = lane & 15, s = Rw % S;
@@ -155,6 +162,7 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     } else {
       yp[lane] = 0; yinc[lane] = 0;
     }
+    ysw[lane] = (cl && kdelay[kc] < p) ? kdelay[kc] : -1;
     all[lane] = true;
   }
   long extra = 0, steps = 0;
@@ -217,6 +225,7 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     for (int l = 0; l < 64; ++l) {
       if (r == rsw[l]) { rq[l] = rline[l]; rinc[l] = NY; }
       if (r == wsw[l]) { wq[l] = dump[l]; winc[l] = 0; }
+      if (r == ysw[l]) { yp[l] = 0; yinc[l] = 0; }  // the zero slots
     }
   }
   return steps ? (double)extra / steps : 0.0;
@@ -244,22 +253,25 @@ uint64_t lcg(uint64_t& s) {
 
 }  // namespace
 
-// Workgroup size of the row kernel for layout R.  Four waves, unless two-wave
-// workgroups hold >= 1.5x the resident waves (a workgroup's waves go to
-// SIMDs in a fixed cyclic order, so small workgroups can pile onto a SIMD;
-// measured at p = 100: par-coop 6 vs 4 waves 0.72 vs 0.80 ms, ser-cent at
-// equal waves 0.68 vs 0.54 ms, one-wave workgroups slower still).  0 when
-// fewer than 4 waves per CU fit (one per SIMD): the one-QP-per-wave kernel
-// is faster there (cent p = 200: 1.36 vs 2.06 ms).  CMPC_ROWS_WPG=4|2
-// overrides it for timing.
+// Workgroup size of the row kernel for layout R: four waves wherever at
+// least one four-wave workgroup per CU fits; two-wave workgroups only where
+// they hold twice the resident waves.  A workgroup's waves go to SIMDs in a
+// fixed cyclic order, so small workgroups pile onto some SIMDs: at p = 100
+// (round 2, w tables of D + 3 entries) four-wave workgroups measured as fast
+// or faster in every case (par-coop 8 vs 6 waves 0.52 vs 0.68 ms, par-cent
+// 8 vs 8 waves 0.290 vs 0.290 ms, ser-coop 4 vs 6 waves 0.89 vs 1.41 ms,
+// ser-cent 4 vs 6 waves 0.49 vs 0.80 ms; tools/gpu_wpg_sweep.sh).  0 when
+// not even one two-wave workgroup per SIMD fits: the one-QP-per-wave kernel
+// runs.  CMPC_ROWS_WPG=4|2 overrides it for timing.
 int cmpc_rows_waves_per_group(const RowsLayout& R) {
   if (const char* e = std::getenv("CMPC_ROWS_WPG")) {
     const int w = std::atoi(e);
     if ((w == 4 || w == 2) && waves_with(R, w) > 0) return w;
   }
   const int w4 = waves_with(R, 4), w2 = waves_with(R, 2);
-  if (2 * w2 >= 3 * w4 && w2 >= 4) return 2;
-  return w4 >= 4 ? 4 : 0;
+  if (w2 >= 2 * w4 && w2 >= 4) return 2;
+  if (w4 >= 4) return 4;
+  return w2 >= 4 ? 2 : 0;
 }
 
 void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out) {

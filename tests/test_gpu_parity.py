@@ -104,7 +104,8 @@ def test_gpu_build_matches_oracle(plant, ctype, p, variant):
 
 @pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "cent", 50),
                                            ("ser", "coop", 100), ("par", "coop", 20),
-                                           ("par", "coop", 100)])
+                                           ("par", "coop", 100), ("par", "cent", 200),
+                                           ("ser", "cent", 100)])
 def test_gpu_build_variants_agree_large(plant, ctype, p):
     """Row-layout vs one-QP-per-wave build on a large batch (persistent grid,
     several groups per wave): H, f, G agree to FP64 reassociation.  par-coop
@@ -359,16 +360,17 @@ def test_gpu_survey_config(plant, ctype, p, B, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ctype,p,expect", [("coop", 50, "rows"), ("coop", 100, "rows"),
-                                            ("cent", 200, "wave")])
-def test_gpu_build_auto_selects_kernel(ctype, p, expect):
+@pytest.mark.parametrize("ctype,p,B,expect", [("coop", 50, 4096, "rows"), ("coop", 100, 4096, "rows"),
+                                              ("cent", 200, 8192, "rows"), ("coop", 50, 64, "wave"),
+                                              ("cent", 200, 1024, "wave")])
+def test_gpu_build_auto_selects_kernel(ctype, p, B, expect):
     """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel wherever its LDS fits
-    and the one-QP-per-wave kernel past that (cent p = 200); DESIGN.md §3.0."""
+    and the batch gives it a wave per SIMD, and the one-QP-per-wave kernel for
+    small batches (SURVEY config 5: cent p = 200, 1 024 QPs); DESIGN.md §3.0."""
     _, setup, _, _ = setup_for("par", ctype)
     cfg = cmpc.reference_config("par", ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
-    B = 64
-    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=5)
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=5, n_distinct=min(B, 256))
     with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
         ctx.build()
         got = ctx.last_build_kernel()

@@ -50,7 +50,8 @@ def layout(d, over=None):
     # least the four staged records (rows_layout.cpp make_layout)
     L["ch_off"] = 4 * L["LQ"]
     L["w_off"] = L["ch_off"] + 4 * ny * 16 + over.get("pad_w", 0)
-    L["WL"] = up(p + 2 + U, 2) + over.get("pad_WL", 0)
+    # w lines end at D + 3 entries (the carriers read the zero slots from r = D)
+    L["WL"] = up(min(p + 2 + U, max(d["delay"]) + 3), 2) + over.get("pad_WL", 0)
     L["per_wave"] = max(up(L["w_off"] + 4 * d["nd"] * L["WL"], 2), up(4 * d["rec_len"], 2)) + over.get("pad_wave", 0)
     L["yls"] = p + U + over.get("pad_yls", 0)
     L["yl_off"] = 16 + over.get("pad_yl", 0)
@@ -145,6 +146,10 @@ def simulate(d, L, wave=0, verbose=False):
             ws = dump
         winc0 = ES if (wdel and p - dm > 0) else 0
         wsw = p - dm if (wdel and p - dm > 0) else -1
+        ysw = -1
+        if cl:  # carriers read the zero slots from the segment r = D of their input on
+            kdelay = [D for D in d["delay"] if D > 0]
+            ysw = kdelay[kc] if kdelay[kc] < p else -1
         if st:
             yp, yinc = 0, 0
         elif ol:
@@ -156,7 +161,7 @@ def simulate(d, L, wave=0, verbose=False):
         # every lane stores each step: lanes without the role into the dump area
         lanes.append(dict(mk=mk, ol=ol, zq=(ql + L["z_off"] + oo) if ol else dump, tl=(M > 1 and mk and dm == 0),
                           tq=ql + L["lo"][cm], rq=rs, rinc=0, rline=rline, rsw=rsw,
-                          wq=ws, winc=winc0, wsw=wsw, dump=dump, yp=yp, yinc=yinc))
+                          wq=ws, winc=winc0, wsw=wsw, dump=dump, yp=yp, yinc=yinc, ysw=ysw))
     tot = defaultdict(int)
     ideal = defaultdict(int)
     nsteps = 0
@@ -204,6 +209,8 @@ def simulate(d, L, wave=0, verbose=False):
                 ln["rq"], ln["rinc"] = ln["rline"], ES
             if r == ln["wsw"]:
                 ln["wq"], ln["winc"] = ln["dump"], 0
+            if r == ln["ysw"]:
+                ln["yp"], ln["yinc"] = 0, 0  # the zero slots
     extra = {k: (tot[k] - ideal[k]) / nsteps for k in tot}
     return extra, sum(extra.values())
 
