@@ -539,6 +539,7 @@ void cmpc_solve_kernel(SolveParams P) {
     qp.lbA[c] = cfg[P.co.rlower + c];
     qp.ubA[c] = cfg[P.co.rupper + c];
   }
+  qp.tolerances();
   const bool pd = hinv_of<N>(H, qp.Hinv);
   double hmax = 0.0;
 #pragma unroll
@@ -644,6 +645,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
     qp.lbA[a] = P.lbA[(size_t)q * N + a];
     qp.ubA[a] = P.ubA[(size_t)q * N + a];
   }
+  qp.tolerances();
   const bool pd = hinv_of<N>(H, qp.Hinv);
   double hmax = 0.0;
 #pragma unroll

@@ -51,6 +51,7 @@ void cmpc_coupled_kernel(CoupledParams P) {
     qp.lbA[c] = cfg[P.co.rlower + c];
     qp.ubA[c] = cfg[P.co.rupper + c];
   }
+  qp.tolerances();
   const bool pd = hinv_of<N>(H, qp.Hinv);
   double hmax = 0.0;
 #pragma unroll

@@ -49,6 +49,23 @@ struct Qp {
   static_assert(NB == N || NB == NU, "bounds: general or NU-periodic");
   HS Hinv;
   double lb[NB], ub[NB], lbA[NB], ubA[NB];
+  // phase-B violation thresholds -TOL_P (1 + |beta|) per bound and side,
+  // fixed per QP (tolerances() after the bounds are set), so that the K
+  // Jacobi solves of a QP do not recompute them in every scan
+  double tlb[NB], tub[NB], tlbA[NB], tubA[NB];
+  CMPC_HD void tolerances() {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      tlb[i] = -TOL_P * (1.0 + fabs(lb[i]));
+      tub[i] = -TOL_P * (1.0 + fabs(-ub[i]));
+      tlbA[i] = -TOL_P * (1.0 + fabs(lbA[i]));
+      tubA[i] = -TOL_P * (1.0 + fabs(-ubA[i]));
+    }
+  }
+  CMPC_HD double thr(int j, int side) const {
+    if (j < N) return side ? sel<NB>(tub, j % NB) : sel<NB>(tlb, j % NB);
+    return side ? sel<NB>(tubA, (j - N) % NB) : sel<NB>(tlbA, (j - N) % NB);
+  }
   CMPC_HD double lbv(int j) const { return sel<NB>(lb, j % NB); }
   CMPC_HD double ubv(int j) const { return sel<NB>(ub, j % NB); }
 
@@ -406,7 +423,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         for (int sd = 0; sd < 2; ++sd) {
           const double b = q.beta(j, sd);
           const double sl = q.nu_dot(j, sd, x) - b;
-          if (sl < -TOL_P * (1.0 + fabs(b)) && (pj < 0 || sl < pv)) {
+          if (sl < q.thr(j, sd) && (pj < 0 || sl < pv)) {
             pj = j;
             ps = sd;
             pv = sl;
@@ -522,14 +539,14 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   o.ws = w;
   if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && fact_ok) ? w : kWsInvalid;
   if (o.status == CMPC_QP_OK) {
-    // variables at an active bound are fixed exactly at it
+    // variables at an active bound are fixed exactly at it; the bound
+    // constraints are bits j < N of the working-set word (side at 16 + j),
+    // each j at most once, so per variable one select instead of a loop over
+    // the slots' runtime indices
+    const uint32_t bnd = w & ((1u << N) - 1u), up = (w >> 16) & bnd;
 #pragma unroll
-    for (int a = 0; a < N; ++a)
-      if (a < W.K && W.j[a] < N) {
-#pragma unroll
-        for (int r = 0; r < N; ++r)
-          if (r == W.j[a]) x[r] = W.side[a] ? q.ubv(r) : q.lbv(r);
-      }
+    for (int r = 0; r < N; ++r)
+      x[r] = ((bnd >> r) & 1u) ? (((up >> r) & 1u) ? q.ubv(r) : q.lbv(r)) : x[r];
   } else {
 #pragma unroll
     for (int r = 0; r < N; ++r) x[r] = 0.0;

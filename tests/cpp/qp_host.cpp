@@ -16,6 +16,7 @@ static void run(const double* Hp, const double* gp, const double* lb, const doub
     g[a] = gp[a];
     qp.lb[a] = lb[a]; qp.ub[a] = ub[a]; qp.lbA[a] = lbA[a]; qp.ubA[a] = ubA[a];
   }
+  qp.tolerances();
   const bool pd = hinv_of<N>(H, qp.Hinv);
   double hmax = 0.0;
   for (int i = 0; i < N; ++i) hmax = fabs(H[i][i]) > hmax ? fabs(H[i][i]) : hmax;
