@@ -287,6 +287,63 @@ def test_gpu_large_batch_properties():
                                atol=1e-10)
 
 
+def test_gpu_max_batch_64bit_offsets():
+    """Maximum-size case: 2^20 scenarios (2 097 152 QPs; 5.2 GB of lin records
+    on the device, so byte offsets pass 2^32 and QP indices 2^21), records made
+    by the device producer from 1 024 distinct operating points and u_old
+    rows tiled with the same period.  Every QP must equal its first copy bit
+    for bit (H, f, G, the plans, status and working sets: an index or offset
+    overflow anywhere in the batch breaks that), and the last scenarios must
+    match the oracle."""
+    import torch
+    from cmpc.synthetic import synthetic_operating_points, synthetic_u_old
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B, nd, S, n = 1 << 20, 1024, cfg.S, cfg.nV
+    xs, us, ys = synthetic_operating_points(cfg, B, seed=2024, n_distinct=nd)
+    u_nd = synthetic_u_old(cfg, nd, np.random.default_rng(2025))
+    u_old = np.ascontiguousarray(np.tile(u_nd, (B // nd, 1)))
+    tx, tu, ty = (torch.from_numpy(a).cuda() for a in (xs, us, ys))
+    with cmpc.Context(cfg, B) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u_old, np.zeros((B * S, n)), np.zeros(B * S, np.uint32))
+        ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+        ctx.build()
+        assert ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS
+        H, f, G = ctx.download_qp()
+        ctx.init_warmstart()
+        ctx.iterate(9)
+        du, st, nw = ctx.download()
+        _, _, ws = ctx.get_state()
+    per = nd * S  # QPs per period
+    for a in (H, f, G, du, st, nw, ws):
+        v = a.reshape(B * S // per, per, -1)
+        assert np.array_equal(v, np.broadcast_to(v[:1], v.shape)), "copies differ"
+    assert (st == 0).all()
+    # the last eight scenarios against the oracle (records from the host producer)
+    last = np.arange(B - 8, B)
+    dims1 = CmpcDims.from_config(cfg, 1)
+    L = cmpc.layout_of(dims1)
+    lin_s = np.zeros((len(last) * S, L.rec_len))
+    for i, b in enumerate(last):
+        for s_ in range(S):
+            r = lin_s[i * S + s_]
+            cmpc.plant_lin_record(cfg, dims1, s_, xs[b], us[b], out=r)
+            r[L.off_y:L.off_y + cfg.ny] = ys[b][cfg.out_idx[s_]]
+    qs = (last[:, None] * S + np.arange(S)[None, :]).reshape(-1)
+    u_s = np.ascontiguousarray(u_old[qs])
+    Ho, fo, Go = oracle_qps(cfg, arr, lin_s, u_s)
+    for i, q in enumerate(qs):
+        sH = np.abs(Ho[i]).max()
+        np.testing.assert_allclose(H[q], Ho[i], rtol=0, atol=1e-11 * sH)
+        np.testing.assert_allclose(f[q], fo[i], rtol=0, atol=1e-10 * max(np.abs(fo[i]).max(), 1e-6 * sH))
+    sub = CmpcDims.from_config(cfg, len(last))
+    odu, ost, *_ = O.step(sub, arr, lin_s, 9, u_s.copy(), np.zeros((len(qs), n)),
+                          np.zeros(len(qs), np.uint32), init=True)
+    np.testing.assert_allclose(du[qs], odu, rtol=1e-9, atol=1e-10)
+
+
 def test_gpu_full_batch_kkt():
     """At the bench size (coop-par p=50, B=65536, 131 072 QPs) every QP the
     device solves is the QP optimum: a KKT certificate (feasibility, tight
