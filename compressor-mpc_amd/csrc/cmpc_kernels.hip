@@ -576,7 +576,7 @@ void cmpc_solve_kernel(SolveParams P) {
     double fk[N];
 #pragma unroll
     for (int a = 0; a < N; ++a) fk[a] = f[a];
-    if (NVO > 0) {
+    if (NVO > 0 && CMPC_QP_ABL != 3) {
       double dother[NVOA];
 #pragma unroll
       for (int rk = 0; rk < SM1; ++rk) {

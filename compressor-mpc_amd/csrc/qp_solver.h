@@ -19,6 +19,9 @@
 // Warm-started dual active-set QP solver (lane per QP).  Same specification
 // and arithmetic order as oracle/or_qp.c; see DESIGN.md §QP.
 // ---------------------------------------------------------------------------
+#ifndef CMPC_QP_ABL
+#define CMPC_QP_ABL 0  // timing-only ablations (results invalid): 1 no phase B, 2 no phase A solve
+#endif
 #define TOL_P 1e-12
 #define TOL_D 1e-12
 #define TOL_R 1e-12
@@ -370,6 +373,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     for (int a = 0; a < N; ++a)
       rhs[a] = (a < W.K) ? W.bta[a] - ndot<N>(W.nrm[a], xu) : 0.0;
     ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
+    if (CMPC_QP_ABL == 2) break;
     int worst = -1;
     double wv = -tol_d;
 #pragma unroll
@@ -409,7 +413,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     }
   }
   // B. Goldfarb–Idnani
-  for (int outer = 0; outer <= max_chg + 1 && !done; ++outer) {
+  for (int outer = 0; outer <= max_chg + 1 && !done && CMPC_QP_ABL != 1; ++outer) {
     int pj = -1, ps = 0;
     double pv = 0.0;
     uint32_t act = 0;
