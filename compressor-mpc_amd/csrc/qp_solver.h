@@ -420,20 +420,32 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
 #pragma unroll
     for (int a = 0; a < N; ++a)
       if (a < W.K) act |= 1u << W.j[a];
+    // the violated candidates first, branch-free: in most scans there are
+    // none, and the ordered selection below (the most violated, first in
+    // (j, side) order on ties) is skipped
+    uint32_t viol = 0;
 #pragma unroll
-    for (int j = 0; j < 2 * N; ++j) {
-      if (!((act >> j) & 1u)) {
+    for (int j = 0; j < 2 * N; ++j)
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        const double sl = q.nu_dot(j, sd, x) - q.beta(j, sd);
+        viol |= (sl < q.thr(j, sd) ? 1u : 0u) << (2 * j + sd);
+      }
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j)
+      if ((act >> j) & 1u) viol &= ~(3u << (2 * j));
+    if (viol) {
+#pragma unroll
+      for (int j = 0; j < 2 * N; ++j)
 #pragma unroll
         for (int sd = 0; sd < 2; ++sd) {
-          const double b = q.beta(j, sd);
-          const double sl = q.nu_dot(j, sd, x) - b;
-          if (sl < q.thr(j, sd) && (pj < 0 || sl < pv)) {
+          const double sl = q.nu_dot(j, sd, x) - q.beta(j, sd);
+          if (((viol >> (2 * j + sd)) & 1u) && (pj < 0 || sl < pv)) {
             pj = j;
             ps = sd;
             pv = sl;
           }
         }
-      }
     }
     if (pj < 0) break;  // optimal
     double np_[N];
