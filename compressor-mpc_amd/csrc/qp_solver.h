@@ -416,36 +416,36 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   for (int outer = 0; outer <= max_chg + 1 && !done && CMPC_QP_ABL != 1; ++outer) {
     int pj = -1, ps = 0;
     double pv = 0.0;
-    uint32_t act = 0;
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-      if (a < W.K) act |= 1u << W.j[a];
-    // the violated candidates first, branch-free: in most scans there are
-    // none, and the ordered selection below (the most violated, first in
-    // (j, side) order on ties) is skipped
-    uint32_t viol = 0;
-#pragma unroll
-    for (int j = 0; j < 2 * N; ++j)
-#pragma unroll
-      for (int sd = 0; sd < 2; ++sd) {
-        const double sl = q.nu_dot(j, sd, x) - q.beta(j, sd);
-        viol |= (sl < q.thr(j, sd) ? 1u : 0u) << (2 * j + sd);
-      }
+    // any violated candidate at all (the compares feed one lane mask, no
+    // per-candidate VALU bookkeeping): in most scans there is none, and the
+    // ordered selection below (the most violated inactive constraint, first
+    // in (j, side) order on ties) is skipped.  An active constraint whose
+    // slack rounds below the threshold only sends the lane to the selection,
+    // which excludes it as before.
+    bool anyv = false;
 #pragma unroll
     for (int j = 0; j < 2 * N; ++j)
-      if ((act >> j) & 1u) viol &= ~(3u << (2 * j));
-    if (viol) {
 #pragma unroll
-      for (int j = 0; j < 2 * N; ++j)
+      for (int sd = 0; sd < 2; ++sd) anyv = anyv | (q.nu_dot(j, sd, x) - q.beta(j, sd) < q.thr(j, sd));
+    if (anyv) {
+      uint32_t act = 0;
 #pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          const double sl = q.nu_dot(j, sd, x) - q.beta(j, sd);
-          if (((viol >> (2 * j + sd)) & 1u) && (pj < 0 || sl < pv)) {
-            pj = j;
-            ps = sd;
-            pv = sl;
+      for (int a = 0; a < N; ++a)
+        if (a < W.K) act |= 1u << W.j[a];
+#pragma unroll
+      for (int j = 0; j < 2 * N; ++j) {
+        if (!((act >> j) & 1u)) {
+#pragma unroll
+          for (int sd = 0; sd < 2; ++sd) {
+            const double sl = q.nu_dot(j, sd, x) - q.beta(j, sd);
+            if (sl < q.thr(j, sd) && (pj < 0 || sl < pv)) {
+              pj = j;
+              ps = sd;
+              pv = sl;
+            }
           }
         }
+      }
     }
     if (pj < 0) break;  // optimal
     double np_[N];
