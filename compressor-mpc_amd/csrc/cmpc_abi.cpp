@@ -97,6 +97,7 @@ struct cmpc_ctx {
   double *d_obsM = nullptr, *obs = nullptr;
   double* stage = nullptr;  // host-pointer observer calls: device staging
   size_t stage_cap = 0;
+  int64_t obs_steps = 0;  // a-priori steps since cmpc_observer_init: the delay blocks' ring phase
   int obs_io[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS] = {};
   int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
   // build kernel selection (cmpc_set_build_variant)
@@ -559,6 +560,7 @@ static void observer_params(cmpc_ctx* c, ObserverParams* P) {
     if (d.delay[i]) {
       P->dinput[P->nd] = i;
       P->blk[P->nd] = blk;
+      P->rot[P->nd] = d.delay[i] > 1 ? (int)(c->obs_steps % (d.delay[i] - 1)) : 0;
       blk += d.delay[i] - 1;
       P->nd++;
     }
@@ -586,8 +588,7 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
     return fail("cmpc_set_observer: n_outputs differs between sub-controllers");
   if (c->L.nobs > 32) return fail("cmpc_set_observer: ns + ndist > 32");
   if (cmpc_obs_prior_shape(c->L.ntot - c->L.nobs, c->L.nd, d.nu_tot) <= 0)
-    return fail("cmpc_set_observer: " + std::to_string(c->L.ntot - c->L.nobs) +
-                " delay-block states per QP exceed the a-priori kernel's budget of 256 (sum of input delays)");
+    return fail("cmpc_set_observer: more than 16 inputs or delayed inputs per sub-controller");
   for (int i = 0; i < d.nu_tot; ++i)
     if (d.delay[i] == 1) return fail("cmpc_set_observer: a one-step input delay has no delay block");
   HIP_TRY(hipSetDevice(c->device));
@@ -621,6 +622,16 @@ static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) 
   if (fill_produce(c, "observer", c->obs_plant, c->obs_pin, c->obs_pout, c->obs_Ts, io, oi, &P, &no))
     return -1;
   P.per_qp = 1;
+  {  // the observer rows' delay blocks are rings (cmpc_obs_prior_kernel)
+    ObserverParams O;
+    observer_params(c, &O);
+    P.nring = O.nd;
+    for (int k = 0; k < O.nd && k < CMPC_ND_MAX; ++k) {
+      P.rb[k] = O.blk[k] - c->d.ns;  // dx index -> dx_aug tail index
+      P.rlen[k] = O.delay[O.dinput[k]] - 1;
+      P.rot[k] = O.rot[k];
+    }
+  }
   P.x = c->obs;
   P.x_stride = c->obs_len;
   P.dx_aug = c->obs + c->d.ns + c->d.ns;  // dx_aug tail (aug states) of slot 0
@@ -656,6 +667,7 @@ int cmpc_observer_init(cmpc_ctx* c, int plant, double p_in, double p_out, double
   }
   HIP_TRY(hipSetDevice(c->device));
   if (observer_upload_M(c)) return -1;
+  c->obs_steps = 0;  // the rings start in logical order
   ObserverParams P;
   observer_params(c, &P);
   P.x_init = x_init;
@@ -689,7 +701,9 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   observer_params(c, &P);
   if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream))
     return fail("cmpc_observe_apply: no a-priori kernel instantiation for these dimensions");
-  return check_launch("observer a-priori kernel");
+  if (check_launch("observer a-priori kernel")) return -1;
+  c->obs_steps++;  // the delay-block rings advance by one
+  return 0;
 }
 
 // copies host arrays (nullptr entries skipped) into the context's staging
@@ -977,13 +991,36 @@ int cmpc_accumulate_moves(cmpc_ctx* c, const int32_t* input_order, double* u_con
   return check_launch("accumulate kernel");
 }
 
+// Rows between the device layout (delay blocks as rings, rotated by the
+// a-priori step count, cmpc_obs_prior_kernel) and the logical layout of the
+// ABI (observer.h's AugmentedState order).  to_logical: device -> logical.
+static void observer_rows_rotate(cmpc_ctx* c, const double* in, double* out, bool to_logical) {
+  ObserverParams O;
+  observer_params(c, &O);
+  const size_t n = (size_t)c->nqp, len = c->obs_len;
+  std::memcpy(out, in, sizeof(double) * n * len);
+  for (int k = 0; k < O.nd; ++k) {
+    const int L = O.delay[O.dinput[k]] - 1, r = O.rot[k];
+    if (L < 2 || r == 0) continue;
+    const size_t b0 = (size_t)c->d.ns + O.blk[k];  // row offset of the block (after x_hat)
+    for (size_t q = 0; q < n; ++q)
+      for (int i = 0; i < L; ++i) {
+        const size_t phys = b0 + (i + r) % L, logi = b0 + i;
+        if (to_logical) out[q * len + logi] = in[q * len + phys];
+        else out[q * len + phys] = in[q * len + logi];
+      }
+  }
+}
+
 int cmpc_get_observer_state(cmpc_ctx* c, double* host) {
   if (!c || !host) return fail("null argument");
   if (!c->obs) return fail("no observer state (cmpc_set_observer)");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemcpyAsync(host, c->obs, sizeof(double) * (size_t)c->nqp * c->obs_len,
-                         hipMemcpyDeviceToHost, c->stream));
+  std::vector<double> dev((size_t)c->nqp * c->obs_len);
+  HIP_TRY(hipMemcpyAsync(dev.data(), c->obs, sizeof(double) * dev.size(), hipMemcpyDeviceToHost,
+                         c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  observer_rows_rotate(c, dev.data(), host, true);
   return 0;
 }
 
@@ -991,8 +1028,10 @@ int cmpc_set_observer_state(cmpc_ctx* c, const double* host) {
   if (!c || !host) return fail("null argument");
   if (!c->obs) return fail("no observer state (cmpc_set_observer)");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemcpyAsync(c->obs, host, sizeof(double) * (size_t)c->nqp * c->obs_len,
-                         hipMemcpyHostToDevice, c->stream));
+  std::vector<double> dev((size_t)c->nqp * c->obs_len);
+  observer_rows_rotate(c, host, dev.data(), false);
+  HIP_TRY(hipMemcpyAsync(c->obs, dev.data(), sizeof(double) * dev.size(), hipMemcpyHostToDevice,
+                         c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
 }

@@ -134,6 +134,10 @@ struct ProduceParams {
   // output matrix (n_outputs x ns) stored to c_out + q * c_stride
   int per_qp, x_stride, dx_stride, c_stride;
   double* c_out;
+  // per-QP mode: dx_aug's delay blocks are rings (observer.hip): block k
+  // spans dx_aug entries [rb[k], rb[k] + rlen[k]), logical entry i stored at
+  // rb[k] + (i + rot[k]) mod rlen[k]
+  int nring, rb[CMPC_ND_MAX], rlen[CMPC_ND_MAX], rot[CMPC_ND_MAX];
 };
 
 // Observer kernels (observer.hip)
@@ -154,6 +158,7 @@ struct ObserverParams {
   int delay[CMPC_MAX_INPUTS];   // per input (sub-controller order)
   int dinput[CMPC_MAX_INPUTS];  // k-th delayed input -> input index
   int blk[CMPC_MAX_INPUTS];     // first dx index of delay block k
+  int rot[CMPC_MAX_INPUTS];     // ring position of block k's first state (step count mod D - 1)
 };
 
 // One Jacobi iteration of the sub-controller-sharded cooperative loop

@@ -98,29 +98,30 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_post_kernel(ObserverPara
   if (l < NO) yo[l] = yl;
 }
 
-// a priori + u_old update: QPW QPs per wave side by side, one per
-// 64/QPW-lane group (the delay blocks span ntot - nobs = 80 entries for the
-// reference plants, KH per lane).  The kernel is bound by load latency x
-// rounds of resident waves: observe_apply for 131k QPs measured 0.113 ms at
-// one QP per wave, 0.091 at two, 0.085 at four; several QPs looped per wave
-// were slower (0.136 ms).  The launcher picks the most QPs per wave whose
-// lanes hold every aug entry (cmpc_obs_prior_shape).  Every source value is
-// loaded before any store.
-template <int NS, int NUT, int QPW, int KH>
+// a priori + u_old update, four QPs per wave (one 16-lane row each).
+// The delay blocks of dx are rings: block k's logical state i (i < D - 1,
+// D its input's delay) is stored at blk[k] + (i + rot[k]) mod (D - 1), with
+// rot the number of a-priori steps since cmpc_observer_init.  The reference's
+// shift (AComposite::Aaug: slot k <- the block's first state, a state <- its
+// successor, the last state <- du' of the input, BComposite::Baug) is then a
+// read of the first state and a write of du' over it, the ring advancing by
+// one: 4 + 2 nd entries per QP written instead of the whole aug part (78 for
+// the reference plants).  cmpc_get/set_observer_state present the rows in
+// the logical order.  Every source value is loaded before any store.
+template <int NS, int NUT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverParams P) {
-  constexpr int kLq = 64 / QPW;  // lanes per QP
-  constexpr int kH = KH;         // aug entries per lane: kLq * kH >= ntot - nobs (launcher)
-  static_assert(kLq >= NS && kLq >= NUT, "a QP's lane group holds a state row per lane and every input");
-  const int lane = threadIdx.x & (kLq - 1), base = threadIdx.x & (64 - kLq);
+  static_assert(NS <= 16 && NUT <= 16, "a QP's 16-lane row holds a state row per lane and every input");
+  const int lane = threadIdx.x & 15, base = threadIdx.x & 48;
   const int nobs = P.nobs, nd = P.nd;
   // delay tables in registers (compile-time indices: a runtime-indexed
   // kernel-argument read is a dependent memory load)
-  int dl[NUT], din[NUT], blk[NUT];
+  int dl[NUT], din[NUT], blk[NUT], rot[NUT];
 #pragma unroll
   for (int i = 0; i < NUT; ++i) {
     dl[i] = P.delay[i];
     din[i] = P.dinput[i];
     blk[i] = P.blk[i];
+    rot[i] = P.rot[i];
   }
   auto pick = [](const int* a, int k) {
     int v = a[0];
@@ -128,8 +129,8 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
     return v;
   };
-  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * QPW + base / kLq;
-  const bool valid = q_raw < P.nqp;  // (an idle lane group keeps the wave's shuffles)
+  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4 + (base >> 4);
+  const bool valid = q_raw < P.nqp;  // (an idle row keeps the wave's shuffles)
   const int q = valid ? q_raw : P.nqp - 1;
   double* st = P.obs + (size_t)q * P.obs_len;
   double* dx = st + NS;
@@ -139,40 +140,20 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
   const int li = lane < NUT ? lane : 0;
   const double u0 = uo[li];
   const double du = (lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0;
-  // lanes < nd: delayed-input slot value and its input's u_old
+  // lanes < nd: delayed-input slot, the block's first state (ring head), the
+  // input's u_old
   const int lk = lane < nd ? lane : 0;
+  const int ik = pick(din, lk);
+  const int head = pick(blk, lk) + pick(rot, lk);
   const double slot = dx[nobs + lk];
-  const double useg = uo[pick(din, lk)];
+  const double first = dx[head];
+  const double useg = uo[ik];
   // lanes < ns: row of B (sub-controller input order) and f
   const int ls = lane < NS ? lane : 0;
   double brow[NUT];
 #pragma unroll
   for (int i = 0; i < NUT; ++i) brow[i] = rec[P.off_B + ls * NUT + i];
   const double fl = rec[P.off_f + ls];
-  // aug part: slot k <- first state of block k; a block state <- its
-  // successor; the block's last state <- du' of its input (Baug)
-  double nv[kH];
-  int tgt[kH], from_du[kH];
-#pragma unroll
-  for (int h = 0; h < kH; ++h) {
-    const int e = nobs + lane + kLq * h;
-    tgt[h] = -1;
-    from_du[h] = -1;
-    nv[h] = 0.0;
-    if (e < P.ntot) {
-      tgt[h] = e;
-      if (e < nobs + nd) {
-        nv[h] = dx[pick(blk, e - nobs)];
-      } else {
-        int k = 0;
-#pragma unroll
-        for (int kk = 1; kk < NUT; ++kk) k += (kk < nd && e >= blk[kk]) ? 1 : 0;
-        const int i = pick(din, k);
-        if (e - pick(blk, k) < pick(dl, i) - 2) nv[h] = dx[e + 1];
-        else from_du[h] = i;
-      }
-    }
-  }
   // du' = du + u_old on delayed inputs (AdjustAppliedInput); dx' slots minus
   // u_old (AdjustFirstDelayedStates)
   const double dup = pick(dl, li) ? du + u0 : du;
@@ -195,17 +176,15 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     if (k < nd) tsum += bk * sk;
   }
   const double xn = (bsum + tsum) + fl;
+  double last = dupv[0];  // du' of the block's input: its new last state
+#pragma unroll
+  for (int i = 1; i < NUT; ++i) last = (ik == i) ? dupv[i] : last;
   WAVE_SYNC();  // all loads above have completed before the first store
   if (!valid) return;
   if (lane < NS) dx[lane] = xn;
-#pragma unroll
-  for (int h = 0; h < kH; ++h) {
-    if (tgt[h] < 0) continue;
-    double val = nv[h];
-#pragma unroll
-    for (int i = 0; i < NUT; ++i)
-      if (from_du[h] == i) val = dupv[i];
-    dx[tgt[h]] = val;
+  if (lane < nd) {
+    dx[nobs + lane] = first;  // slot k <- first state of block k
+    dx[head] = last;          // the ring advances: this entry becomes the last state
   }
   // UpdateU: u_old += du (own inputs; the others add zero)
   if (lane < NUT) uo[lane] = u0 + du;
@@ -213,15 +192,12 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
 
 }  // namespace
 
-// QPs per wave of the a-priori kernel for n_aug delay-block entries per QP
-// (lane group of 64/QPW lanes x the instantiation's entries per lane: 16 x 6,
-// 32 x 4, 64 x 4), 0 if none holds them.
+// The a-priori kernel's shape for n_aug delay-block entries per QP: one
+// 16-lane row per QP whatever the delays (the delay blocks are rings, see
+// cmpc_obs_prior_kernel); 0 if a QP's states or inputs do not fit a row.
 int cmpc_obs_prior_shape(int n_aug, int nd, int nu_tot) {
-  if (nd > 16 || nu_tot > 16) return 0;
-  if (n_aug <= 16 * 6) return 4;
-  if (n_aug <= 32 * 4) return 2;
-  if (n_aug <= 64 * 4) return 1;
-  return 0;
+  (void)n_aug;
+  return (nd <= 16 && nu_tot <= 16) ? 4 : 0;
 }
 
 int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
@@ -243,20 +219,15 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       return 0;
     }
     case CMPC_OBS_PRIOR: {
-      const int qpw = cmpc_obs_prior_shape(P.ntot - P.nobs, P.nd, P.nu_tot);
-      if (qpw <= 0) return -1;
-      const int g = (P.nqp + qpw * kWaves - 1) / (qpw * kWaves);
-#define OBS_PRIOR(NS_)                                                                        \
-  switch (qpw) {                                                                              \
-    case 4: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 4, 6>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
-    case 2: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 2, 4>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
-    case 1: hipLaunchKernelGGL((cmpc_obs_prior_kernel<NS_, 4, 1, 4>), dim3(g), dim3(64 * kWaves), 0, s, P); return 0; \
-  }
-      if (P.nu_tot != 4) return -1;
-      if (P.ns == 11) { OBS_PRIOR(11) }
-      if (P.ns == 10) { OBS_PRIOR(10) }
-#undef OBS_PRIOR
-      return -1;
+      if (cmpc_obs_prior_shape(P.ntot - P.nobs, P.nd, P.nu_tot) <= 0 || P.nu_tot != 4) return -1;
+      const int g = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
+      if (P.ns == 11)
+        hipLaunchKernelGGL((cmpc_obs_prior_kernel<11, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
+      else if (P.ns == 10)
+        hipLaunchKernelGGL((cmpc_obs_prior_kernel<10, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
+      else
+        return -1;
+      return 0;
     }
   }
   return -1;

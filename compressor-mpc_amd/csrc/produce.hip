@@ -189,7 +189,16 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + u * kLanes;
-        v[u] = (dx && e < P.naug) ? dx[e] : 0.0;
+        // logical entry e of a ring-stored delay block (observer state,
+        // cmpc_obs_prior_kernel) -> its position in the row
+        int pe = e;
+#pragma unroll
+        for (int k = 0; k < CMPC_ND_MAX; ++k)
+          if (k < P.nring && e >= P.rb[k] && e < P.rb[k] + P.rlen[k]) {
+            const int i = e - P.rb[k] + P.rot[k];
+            pe = P.rb[k] + (i >= P.rlen[k] ? i - P.rlen[k] : i);
+          }
+        v[u] = (dx && e < P.naug) ? dx[pe] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)

@@ -305,6 +305,7 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
     double best_cost = loop_conflicts(d, nd, best, 0);
     Pads bp = base;
     uint64_t seed = 0x5eedULL;
+    if (const char* e = std::getenv("CMPC_ROWS_SEED")) seed = std::strtoull(e, nullptr, 0);  // layout A/B
     for (int it = 0; it < 400 && best_cost > 0.0; ++it) {
       Pads cand = bp;
       const int nchg = 1 + (int)(lcg(seed) % 3);

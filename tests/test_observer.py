@@ -187,8 +187,7 @@ def lin_records(cfg, dims, L, xh, u_full, dx, y):
     ("par", "coop", 96, None), ("ser", "cent", 96, None),
     # B*S not a multiple of the 16 QPs per a-priori workgroup: the tail groups
     ("par", "coop", 37, None), ("ser", "cent", 37, None),
-    # 120 and 140 delay-block states: the two- and one-QP-per-wave a-priori
-    # instantiations (the four-QP one holds 96)
+    # longer delay lines (118 and 138 delay-block states; rings of 59 and 69)
     ("par", "coop", 37, (0, 60, 0, 60)), ("par", "coop", 21, (0, 70, 0, 70))])
 def test_gpu_observer_kernels_match_oracle(plant, ctype, B, delays):
     cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, 20, B, 5, delays=delays)
@@ -243,6 +242,46 @@ def test_gpu_observer_kernels_match_oracle(plant, ctype, B, delays):
             assert np.array_equal(d2[q], dd), q
             assert np.array_equal(u2[q], uo), q
         assert np.array_equal(xh2, xh1)  # x_hat moves only in the a-posteriori step
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("delays,steps", [((0, 5, 0, 7), 30), (None, 83)])
+def test_gpu_observer_delay_rings_wrap(delays, steps):
+    """The delay blocks live on the device as rings rotated by the a-priori
+    step count (cmpc_obs_prior_kernel).  Over enough a-priori steps for every
+    ring to wrap (block lengths 4 and 6 thirty times; the reference's 39 over
+    83 steps) the state equals the oracle's shifted AugmentedState bit for bit
+    at every check, the logical rows survive a get/set round trip, and the
+    per-QP producer's records after the last step carry the logical tail."""
+    B = 21
+    cfg, arr, dims, L, rng, x, u, y, M = setup("par", "coop", 20, B, 11, delays=delays)
+    nq = B * cfg.S
+    dx0 = rng.normal(0, 1e-3, (nq, L.ntot))
+    with cmpc.Context(cfg, B, device=0) as ctx:
+        ctx.configure(arr)
+        for s in range(cfg.S):
+            ctx.set_observer(s, M[s])
+        tx, tu, ty, tdx = dev(x), dev(u), dev(y), dev(dx0)
+        ctx.observer_init(tx.data_ptr(), tu.data_ptr(), ty.data_ptr(), tdx.data_ptr())
+        rec = ctx.download_lin()
+        d = dx0.copy()
+        for t in range(steps):
+            u_old = rng.normal(0, 0.05, (nq, cfg.nu_tot))
+            du_old = rng.normal(0, 0.02, (nq, cfg.nV))
+            ctx.set_state(u_old, du_old, np.zeros(nq, np.uint32))
+            ctx.observe_apply()
+            for q in range(nq):
+                O.observe_prior(dims, rec[q], du_old[q, :cfg.nu], u_old[q].copy(), d[q])
+            if t % 7 == 6 or t == steps - 1:
+                st = ctx.observer_state()
+                _, g_d, _, _ = split(cfg, L, st)
+                assert np.array_equal(g_d, d), t
+                ctx.set_observer_state(st)  # logical rows in, the same rings out
+                assert np.array_equal(ctx.observer_state(), st), t
+        ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+        xh1, d1, _, _ = split(cfg, L, ctx.observer_state())
+        np.testing.assert_allclose(ctx.download_lin(), lin_records(cfg, dims, L, xh1, u, d1, y),
+                                   rtol=1e-11, atol=1e-14)
 
 
 @pytest.mark.gpu
