@@ -52,6 +52,22 @@ def test_layout_rejects_bad_dims():
     assert b"invalid" in load_library().cmpc_last_error()
 
 
+def test_empty_batch_rejected_or_noop():
+    """Edge cases of the batch size: an empty batch is an invalid dimension
+    set (B < 1, like the reference's fixed-size Eigen types, which have no
+    empty controller), and the batched solver returns at once for zero QPs
+    (no device touched: this runs without a GPU)."""
+    cfg = reference_config("par", "coop", p=50)
+    d = CmpcDims.from_config(cfg, 1)
+    d.B = 0
+    from cmpc._abi import CmpcLayout
+    assert load_library().cmpc_layout_of(ctypes.byref(d), ctypes.byref(CmpcLayout())) != 0
+    assert b"invalid" in load_library().cmpc_last_error()
+    z = np.zeros((0, 4))
+    x, st, nchg, ws, tr, ntr = cmpc.qp_solve_batch(np.zeros((0, 4, 4)), z, z, z, z, z, nu=2)
+    assert x.shape == (0, 4) and st.shape == (0,)
+
+
 @pytest.mark.parametrize("plant", [0, 1])
 def test_plant_producer_matches_oracle(plant):
     """cmpc_plant_lin_record (product, host) == or_lin_record (oracle restatement)."""
