@@ -46,6 +46,15 @@ def build_flops(cfg, naug: int, nd: int) -> float:
             2 * p * ny * (ns + naug) + p * ny + 2 * p * ny * nV)
 
 
+def iterate_flops(cfg) -> float:
+    """Algorithmic FLOPs of one Jacobi iteration of one sub-controller
+    (ApplyOtherInput's (p ny)-long products + the plan
+    update; the QP solve itself is not counted, a lower bound)."""
+    p, ny, m, nV = cfg.p, cfg.ny, cfg.m, cfg.nV
+    nuo = cfg.nu_tot - cfg.nu
+    return 2 * p * ny * m * nuo + 2 * p * ny * nV
+
+
 def build_bytes(cfg, L) -> float:
     """Algorithmic HBM bytes of one sub-controller build: its lin record
     (Aorig, Bin, Csel, f, dx_aug, y_prev) + u_old in, the condensed QP out."""
@@ -392,6 +401,20 @@ def main():
             "algorithmic_bytes_per_qp": build_bytes(cfg, L),
             "avg_launch_ms": avg_build_s * 1e3,
             "launches": n_build,
+        },
+        "step_roofline": {
+            "definition": ("SURVEY.md 8(d) path roofline: (F_build + K F_it) algorithmic FLOPs per "
+                           "sub-controller x B*S per GPU / measured step time (max over ranks), "
+                           "against the FP64 peak"),
+            "flops_per_qp_step": f_build + K * iterate_flops(cfg),
+            "achieved": B * S * (f_build + K * iterate_flops(cfg)) / (elapsed_max / args.steps) / 1e12,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s per GPU",
+            "frac": B * S * (f_build + K * iterate_flops(cfg)) / (elapsed_max / args.steps) / 1e12
+                    / FP64_PEAK_TFLOPS,
+            "note": ("F_it counts the reference's per-iteration ApplyOtherInput products; this build "
+                     "forms G = Su'W Su_other once in the build kernel (2 p ny nV nVo FLOPs per QP, "
+                     "not in F_build) and applies it with nV nVo FMAs per iteration"),
         },
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1),
