@@ -271,15 +271,21 @@ def main():
             ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
         ctx.synchronize()
         t_prod = (time.perf_counter() - t0) / reps
+        ctx.enable_timing(True)
         t0 = time.perf_counter()
         for _ in range(reps):
             ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
             ctx.step(K, cmpc.CMPC_APPLY_MOVE)
         ctx.synchronize()
         t_cl = (time.perf_counter() - t0) / reps
+        kms = lambda k: ctx.kernel_time(k)[0] / max(ctx.kernel_time(k)[1], 1)
+        cl_kernels = {"produce": kms(cmpc.CMPC_KERNEL_PRODUCE), "build": kms(cmpc.CMPC_KERNEL_BUILD),
+                      "iterate": kms(cmpc.CMPC_KERNEL_ITERATE)}
+        ctx.enable_timing(False)
         _, st_cl, _ = ctx.download()
         _, _, ws_cl = ctx.get_state()
         closed = {"ms_per_step": t_cl * 1e3, "producer_ms": t_prod * 1e3,
+                  "kernels_ms": cl_kernels,
                   "qp_status_ok_fraction": float((st_cl == 0).mean()),
                   "qp_active_constraint_fraction": float((ws_cl != 0).mean()),
                   "qp_solves_per_s": B * S * K / t_cl,
@@ -321,6 +327,7 @@ def main():
             ctx.set_observer_state(obs_snap)
             ctx.set_state(*state_snap)
             ctx.synchronize()
+            ctx.enable_timing(True)
             t0 = time.perf_counter()
             for _ in range(reps):
                 ctx.observe_step(tu.data_ptr(), ty.data_ptr())
@@ -329,9 +336,14 @@ def main():
                 ctx.observe_apply()
             ctx.synchronize()
             t_full = (time.perf_counter() - t0) / reps
+            obs_kernels = {"observe_post": kms(cmpc.CMPC_KERNEL_OBSERVE_POST),
+                           "produce_per_qp": kms(cmpc.CMPC_KERNEL_PRODUCE),
+                           "build": kms(cmpc.CMPC_KERNEL_BUILD), "iterate": kms(cmpc.CMPC_KERNEL_ITERATE),
+                           "observe_prior": kms(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
+            ctx.enable_timing(False)
             _, st_o, _ = ctx.download()
             closed["with_observer"] = {
-                "ms_per_step": t_full * 1e3, "observe_step_ms": t_os * 1e3,
+                "ms_per_step": t_full * 1e3, "kernels_ms": obs_kernels, "observe_step_ms": t_os * 1e3,
                 "observe_apply_ms": t_oa * 1e3,
                 "qp_status_ok_fraction": float((st_o == 0).mean()),
                 "qp_solves_per_s": B * S * K / t_full,

@@ -16,7 +16,8 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE, CMPC_QP_INFEASIBLE,
+from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE,
+                   CMPC_KERNEL_PRODUCE, CMPC_KERNEL_OBSERVE_POST, CMPC_KERNEL_OBSERVE_PRIOR, CMPC_QP_INFEASIBLE,
                    CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
                    CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
 from .configs import ControllerConfig, SetupFile, reference_config
@@ -294,7 +295,7 @@ class Context:
 
     def enable_timing(self, on: bool = True, only=None):
         """Kernel timing: every kernel (on), none, or only the kernel ids in
-        `only` (CMPC_KERNEL_BUILD / CMPC_KERNEL_ITERATE)."""
+        `only` (CMPC_KERNEL_*)."""
         flag = int(bool(on))
         if on and only is not None:
             flag = 0

@@ -27,6 +27,10 @@ CMPC_TRACE = 2
 
 CMPC_KERNEL_BUILD = 0
 CMPC_KERNEL_ITERATE = 1
+CMPC_KERNEL_PRODUCE = 2
+CMPC_KERNEL_OBSERVE_POST = 3
+CMPC_KERNEL_OBSERVE_PRIOR = 4
+CMPC_KERNEL_COUNT = 5
 
 CMPC_BUILD_AUTO = 0
 CMPC_BUILD_WAVE = 1

@@ -104,11 +104,11 @@ struct cmpc_ctx {
   int build_variant = CMPC_BUILD_AUTO;
   int last_build = 0;  // kernel launched by the last cmpc_build
   // timing
-  int timing = 0;  // bit k: kernel k is timed
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
+  int timing = 0;  // bit k: kernel k (CMPC_KERNEL_*) is timed
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[CMPC_KERNEL_COUNT];
   std::vector<hipEvent_t> event_pool;  // reused so timing stays cheap in a timed loop
-  double tot_ms[2] = {0, 0};
-  int64_t launches[2] = {0, 0};
+  double tot_ms[CMPC_KERNEL_COUNT] = {};
+  int64_t launches[CMPC_KERNEL_COUNT] = {};
 };
 
 namespace {
@@ -203,7 +203,7 @@ int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
 }
 
 int resolve_timing(cmpc_ctx* c) {
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < CMPC_KERNEL_COUNT; ++k) {
     for (auto& pr : c->pending[k]) {
       HIP_TRY(hipEventSynchronize(pr.second));
       float ms = 0;
@@ -332,7 +332,7 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < CMPC_KERNEL_COUNT; ++k)
     for (auto& pr : c->pending[k]) {
       (void)hipEventDestroy(pr.first);
       (void)hipEventDestroy(pr.second);
@@ -526,8 +526,11 @@ int cmpc_produce_lin(cmpc_ctx* c, int plant, double p_in, double p_out, double T
   P.y = y;
   HIP_TRY(hipSetDevice(c->device));
   c->lin_bound = nullptr;  // the build reads the produced records
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_PRODUCE, &e0)) return -1;
   if (cmpc_launch_produce(P, plant, c->stream)) return fail("cmpc_produce_lin: launch failed");
-  return check_launch("produce kernel");
+  if (check_launch("produce kernel")) return -1;
+  return timed_end(c, CMPC_KERNEL_PRODUCE, e0);
 }
 
 // ---- observer ----
@@ -641,8 +644,11 @@ static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) 
   P.u_full = u_full;
   P.y = y;
   c->lin_bound = nullptr;
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_PRODUCE, &e0)) return -1;
   if (cmpc_launch_produce(P, c->obs_plant, c->stream)) return fail("observer: produce launch failed");
-  return check_launch("produce kernel (per QP)");
+  if (check_launch("produce kernel (per QP)")) return -1;
+  return timed_end(c, CMPC_KERNEL_PRODUCE, e0);
 }
 
 int cmpc_observer_init(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
@@ -687,8 +693,11 @@ int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
   ObserverParams P;
   observer_params(c, &P);
   P.y = y;
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_OBSERVE_POST, &e0)) return -1;
   if (cmpc_launch_observer(P, CMPC_OBS_POST, c->stream)) return fail("observer launch failed");
   if (check_launch("observer a-posteriori kernel")) return -1;
+  if (timed_end(c, CMPC_KERNEL_OBSERVE_POST, e0)) return -1;
   return observer_produce(c, u_full, y);
 }
 
@@ -699,11 +708,13 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   ObserverParams P;
   observer_params(c, &P);
+  hipEvent_t e0 = nullptr;
+  if (timed_begin(c, CMPC_KERNEL_OBSERVE_PRIOR, &e0)) return -1;
   if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream))
     return fail("cmpc_observe_apply: no a-priori kernel instantiation for these dimensions");
   if (check_launch("observer a-priori kernel")) return -1;
   c->obs_steps++;  // the delay-block rings advance by one
-  return 0;
+  return timed_end(c, CMPC_KERNEL_OBSERVE_PRIOR, e0);
 }
 
 // copies host arrays (nullptr entries skipped) into the context's staging
@@ -1343,8 +1354,9 @@ int cmpc_download_trace(cmpc_ctx* c, uint8_t* trace, int32_t* ntrace) {
 int cmpc_enable_timing(cmpc_ctx* c, int enable) {
   if (!c) return fail("null context");
   if (resolve_timing(c)) return -1;
-  c->timing = enable == 0 ? 0 : enable == 1 ? 3 : (enable >> 1) & 3;
-  for (int k = 0; k < 2; ++k) {
+  const int all = (1 << CMPC_KERNEL_COUNT) - 1;
+  c->timing = enable == 0 ? 0 : enable == 1 ? all : (enable >> 1) & all;
+  for (int k = 0; k < CMPC_KERNEL_COUNT; ++k) {
     c->tot_ms[k] = 0;
     c->launches[k] = 0;
   }
@@ -1353,7 +1365,7 @@ int cmpc_enable_timing(cmpc_ctx* c, int enable) {
 
 int cmpc_kernel_time(cmpc_ctx* c, int kernel, double* total_ms, int64_t* launches) {
   if (!c) return fail("null context");
-  if (kernel < 0 || kernel > 1) return fail("unknown kernel id");
+  if (kernel < 0 || kernel >= CMPC_KERNEL_COUNT) return fail("unknown kernel id");
   HIP_TRY(hipSetDevice(c->device));
   if (resolve_timing(c)) return -1;
   if (total_ms) *total_ms = c->tot_ms[kernel];

@@ -211,9 +211,9 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
     case CMPC_OBS_POST: {
       const int g4 = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
       if (P.ns == 11 && P.n_out == 4 && P.ndist == 4)
-        hipLaunchKernelGGL((cmpc_obs_post_kernel<11, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
+        cmpc_launch((cmpc_obs_post_kernel<11, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
       else if (P.ns == 10 && P.n_out == 4 && P.ndist == 4)
-        hipLaunchKernelGGL((cmpc_obs_post_kernel<10, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
+        cmpc_launch((cmpc_obs_post_kernel<10, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
       else
         return -1;
       return 0;
@@ -222,9 +222,9 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       if (cmpc_obs_prior_shape(P.ntot - P.nobs, P.nd, P.nu_tot) <= 0 || P.nu_tot != 4) return -1;
       const int g = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
       if (P.ns == 11)
-        hipLaunchKernelGGL((cmpc_obs_prior_kernel<11, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
+        cmpc_launch((cmpc_obs_prior_kernel<11, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
       else if (P.ns == 10)
-        hipLaunchKernelGGL((cmpc_obs_prior_kernel<10, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
+        cmpc_launch((cmpc_obs_prior_kernel<10, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);
       else
         return -1;
       return 0;

@@ -220,11 +220,9 @@ int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream) {
   if (P.S < 1 || P.S > CMPC_MAX_S_PRODUCE || P.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return -1;
   const size_t table = sizeof(int) * (size_t)P.S * P.rec_len;
   if (plant == CMPC_PLANT_PARALLEL)
-    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves),
-                       table, s, P);
+    cmpc_launch(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves), table, s, P);
   else if (plant == CMPC_PLANT_SERIAL)
-    hipLaunchKernelGGL(cmpc_produce_kernel<CMPC_PLANT_SERIAL>, dim3(grid), dim3(64 * kWaves),
-                       table, s, P);
+    cmpc_launch(cmpc_produce_kernel<CMPC_PLANT_SERIAL>, dim3(grid), dim3(64 * kWaves), table, s, P);
   else
     return -1;
   return 0;

@@ -183,7 +183,11 @@ int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
  * opt-in).  enable: 0 off, 1 every kernel, or an OR of CMPC_TIME_ONLY(k)
  * to time only those kernels (the others launch without events). */
 #define CMPC_KERNEL_BUILD 0
-#define CMPC_KERNEL_ITERATE 1
+#define CMPC_KERNEL_ITERATE 1         /* cmpc_iterate, cmpc_coupled_iterate */
+#define CMPC_KERNEL_PRODUCE 2         /* cmpc_produce_lin, the per-QP producer of cmpc_observe_step */
+#define CMPC_KERNEL_OBSERVE_POST 3    /* a posteriori part of cmpc_observe_step */
+#define CMPC_KERNEL_OBSERVE_PRIOR 4   /* cmpc_observe_apply */
+#define CMPC_KERNEL_COUNT 5
 #define CMPC_TIME_ONLY(kernel) (2 << (kernel))
 int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
 int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,

@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
 pmc() {  # name, counters...   (separate passes, kernel trace only)
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-trace -T --kernel-include-regex 'cmpc_build|cmpc_solve' \
+  timeout -k 10 300 rocprofv3 --kernel-trace -T --kernel-include-regex 'cmpc_' \
      --pmc "$@" -d gpurun_out/pmc${TAG}_$name -o run --output-format csv -- \
      python3 bench.py --steps 3 --warmup 1 --no-cpu --settle-seconds 0 > gpurun_out/pmc${TAG}_$name.json 2> gpurun_out/pmc${TAG}_$name.err
 }
