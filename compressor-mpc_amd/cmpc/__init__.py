@@ -20,10 +20,11 @@ from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY
                    CMPC_KERNEL_PRODUCE, CMPC_KERNEL_OBSERVE_POST, CMPC_KERNEL_OBSERVE_PRIOR, CMPC_QP_INFEASIBLE,
                    CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
                    CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
-from .configs import ControllerConfig, SetupFile, reference_config
+from .configs import ControllerConfig, SetupFile, reference_config, reference_observer_gain, reference_setup
 from .problem import ControllerArrays, controller_arrays, plant_input_from_plans
 
-__all__ = ["Context", "ControllerConfig", "SetupFile", "reference_config", "controller_arrays",
+__all__ = ["Context", "ControllerConfig", "SetupFile", "reference_config", "reference_setup",
+           "reference_observer_gain", "controller_arrays",
            "plant_input_from_plans", "plant_lin_record", "plant_default", "plant_output",
            "layout_of", "rows_lds_model", "qp_solve_batch", "CMPC_APPLY_MOVE", "CMPC_TRACE", "CMPC_QP_OK",
            "CMPC_QP_MAX_NWSR", "CMPC_QP_INFEASIBLE", "CMPC_QP_NOT_PD"]

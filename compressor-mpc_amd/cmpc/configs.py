@@ -25,6 +25,7 @@ REF_NDIST = 4
 REF_P = 100
 REF_M = 2
 REF_TS = 0.05  # sampling time of results/*.dat records
+PLANT_N_INPUTS = {PLANT_PARALLEL: 9, PLANT_SERIAL: 8}   # parallel_compressors.h:19, serial_compressors.h:19
 
 
 @dataclass
@@ -103,6 +104,11 @@ class SetupFile:
     constraints_upper: List[float] = field(default_factory=list)
     rate_lower: List[float] = field(default_factory=list)
     rate_upper: List[float] = field(default_factory=list)
+    # `simulation`: segments (plant-input offset change from the default input,
+    # n_inputs numbers; end time in s).  Each segment's offset holds from the
+    # previous segment's end time on (the reference's harness steps the plant
+    # input offset, SimulationSystem::SetOffset, simulation_system.h:64).
+    segments: List[tuple] = field(default_factory=list)
 
     KEYS = ("n-iterations", "n-timing-iterations", "folder-name", "output-filename",
             "yref", "uwt", "ywt", "constraints-lower", "constraints-upper",
@@ -142,33 +148,57 @@ class SetupFile:
         out.constraints_upper = num("constraints-upper")
         out.rate_lower = num("constraints-rate-lower")
         out.rate_upper = num("constraints-rate-upper")
+        sim = num("simulation")
+        ni = PLANT_N_INPUTS[cfg.plant]
+        if len(sim) % (ni + 1):
+            raise RuntimeError(f"simulation: segments of {ni} + 1 numbers expected, got {len(sim)}")
+        out.segments = [(sim[i:i + ni], sim[i + ni]) for i in range(0, len(sim), ni + 1)]
         return out
 
 
 # Run parameters of the reference's setup files (setup/setup-<ctrl>-<plant>,
 # values copied as data; n-iterations is the Jacobi iteration count K).
+# `simulation` blocks: the discharge valve (parallel input 8, default 0.7) and
+# the serial plant's input 6 (default 0.393) step at t = 50 s
+_PAR_SEG = [([0.0] * 9, 50.0), ([0.0] * 8 + [-0.3], 500.0)]
+_SER_SEG = [([0.0] * 8, 50.0), ([0.0] * 6 + [-0.1, 0.0], 500.0)]
 _REF_SETUPS = {
     ("par", "cent"): dict(n_iterations=1, yref=[4.5, 4.5, 0, 1.12],
                           uwt=[2e4, 2e5, 2e4, 2e5], ywt=[[1, 1, 5e2]],
                           lo=[-0.3, 0, -0.3, 0], up=[0.3, 1, 0.3, 1],
-                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1]),
+                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1], seg=_PAR_SEG),
     ("par", "coop"): dict(n_iterations=9, yref=[4.5, 4.5, 0, 1.12],
                           uwt=[1.9e4, 1.9e5, 1.9e4, 1.9e5], ywt=[[1, 1, 4.2e2]] * 2,
-                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1], seg=_PAR_SEG),
     ("par", "ncoop"): dict(n_iterations=9, yref=[4.5, 4.5, 0, 1.12],
                            uwt=[2.2e4, 2.2e5, 2.2e4, 2.2e5], ywt=[[1, 6e2]] * 2,
-                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1], seg=_PAR_SEG),
     ("ser", "cent"): dict(n_iterations=1, yref=[1.030830, 8.125790, 1.187190, 8.125790],
                           uwt=[2e4, 2.5e5, 2e4, 2.5e5], ywt=[[200, 1, 1000, 8]],
                           lo=[-0.3, 0, -0.3, 0], up=[0.3, 1, 0.3, 1],
-                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1]),
+                          rlo=[-0.1] * 4, rup=[0.1, 1, 0.1, 1], seg=_SER_SEG),
     ("ser", "coop"): dict(n_iterations=9, yref=[1.030830, 8.125790, 1.187190, 8.125790],
                           uwt=[4.1e4, 5e5, 2.5e4, 5e5], ywt=[[750, 4, 1500, 8]] * 2,
-                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+                          lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1], seg=_SER_SEG),
     ("ser", "ncoop"): dict(n_iterations=9, yref=[1.030830, 8.125790, 1.187190, 8.125790],
                            uwt=[3e4, 5e5, 3e4, 5e5], ywt=[[1900, 3]] * 2,
-                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1]),
+                           lo=[-0.3, 0], up=[0.3, 1], rlo=[-0.1, -0.1], rup=[0.1, 1], seg=_SER_SEG),
 }
+
+
+def reference_observer_gain(cfg: ControllerConfig, n_outputs: int = 4):
+    """The observer gain M of the reference's runs ((ns + ndist) x n_outputs,
+    one per sub-controller): M = [0; I], the measured output error corrects
+    the disturbance states only, at unit gain.  The gain is set in the
+    harness's missing common-simulation.inc; it is identified from the
+    recorded trajectories (tools/fit_observer_gain.py: every other gain of
+    the form [0; g I] changes u(t) within the first steps), and with it the
+    device closed loop reproduces all 10 000 records of all six reference
+    runs (tests/test_closed_loop_golden.py)."""
+    import numpy as np
+    M = np.zeros((cfg.ns + cfg.ndist, n_outputs))
+    M[cfg.ns:cfg.ns + cfg.ndist, :cfg.ndist] = np.eye(cfg.ndist, min(cfg.ndist, n_outputs))
+    return M
 
 
 def reference_setup(plant: str, controller: str) -> SetupFile:
@@ -182,4 +212,5 @@ def reference_setup(plant: str, controller: str) -> SetupFile:
                      yref=[float(t) for t in v["yref"]], uwt=diag(v["uwt"]),
                      ywt=[diag(w) for w in v["ywt"]], constraints_lower=list(map(float, v["lo"])),
                      constraints_upper=list(map(float, v["up"])),
-                     rate_lower=list(map(float, v["rlo"])), rate_upper=list(map(float, v["rup"])))
+                     rate_lower=list(map(float, v["rlo"])), rate_upper=list(map(float, v["rup"])),
+                     segments=[(list(d), t) for d, t in v["seg"]])

@@ -13,6 +13,18 @@ batched over B scenarios on the device:
     SetInput(u)   -> input delay line -> plant input  simulation_system.h:67-70
     integrate the plant over [t_k, t_k + Ts]          (controlled Dormand-Prince)
 
+  The setup file's `simulation` segments are one Integrate call each, the
+  plant-input offset stepped in between (SetOffset, simulation_system.h:64;
+  the controller keeps its own offset, so the step is an unmeasured
+  disturbance).  integrate_const observes both ends of its interval, so the
+  instant at a segment boundary is observed twice: the last observation of
+  one call (no integration follows), SetOffset, then the first of the next
+  call at the same plant state, whose step-size control starts again from
+  Ts.  The reference's records show exactly that (results/*/run1/*.dat: the
+  records printed at t = 50 and 50.05 hold the same plant state, and every
+  record is one controller call); the record count, not integrate_const's
+  time, labels them.
+
 Everything between two records runs on the GPU (sim.hip, observer.hip,
 produce.hip, cmpc_kernels.hip); torch tensors are the device buffers.
 """
@@ -86,8 +98,23 @@ class ClosedLoop:
         self.x0, self.u_offset = t(x0), t(u_offset)
         self.u_ctrl = torch.zeros(B, cfg.nu_tot, dtype=torch.float64, device=dev)  # NerveCenter::u_old_
         self.u_lin = torch.zeros_like(self.u_offset)   # GetPlantInput(u_old_, u_offset_)
+        self.cidx = torch.tensor(REF_CONTROL_INDEX, dtype=torch.long, device=dev)
         self.io = np.ascontiguousarray(cfg.input_order, dtype=np.int32)
         self.k = 0
+        self._sched = []   # pending (t_start, plant-input offset (B, n_inputs) device)
+
+    def set_segments(self, segments, u_default):
+        """The setup file's `simulation` segments ([(offset change, end time)],
+        SetupFile.segments) over the plant's default input u_default: segment 0's
+        offset is the initial one (call before initialize); segment i's is set
+        after the last instant of segment i-1 (its end time), which no
+        integration follows (module docstring)."""
+        torch = self.torch
+        u_default = np.asarray(u_default, dtype=np.float64)
+        offs = [np.tile(u_default + np.asarray(d, dtype=np.float64), (self.B, 1)) for d, _ in segments]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
+        self.u_offset = t(offs[0])
+        self._sched = [(float(segments[i - 1][1]), t(offs[i])) for i in range(1, len(segments))]
 
     def initialize(self, dx_init=None):
         """SimulationSystem(x0, u_offset) + NerveCenter::Initialize(x0, 0,
@@ -110,17 +137,25 @@ class ClosedLoop:
         torch = self.torch
         t = 0.0 + self.k * self.Ts   # integrate_const: t0 + step * dt
         y = self.sim.output()
-        # GetNextInputWithTiming(y): linearisation input GetPlantInput(u_old_, u_offset_)
-        self.sim.plant_input(self.u_ctrl, self.u_lin)
+        # GetNextInputWithTiming(y): linearisation input GetPlantInput(u_old_,
+        # u_offset_) with the controller's own offset (fixed at Initialize; the
+        # plant's may have stepped, see set_segments)
+        self.u_lin.copy_(self.u_offset)
+        self.u_lin[:, self.cidx] += self.u_ctrl
         self.ctx.observe_step(self.u_lin.data_ptr(), y.data_ptr())
         self.ctx.build()
         self.ctx.iterate(self.K)
         self.ctx.observe_apply()
         check(self.ctx.lib.cmpc_accumulate_moves(self.ctx._h, iptr(self.io),
                                                  self.torch_ptr(self.u_ctrl)), "cmpc_accumulate_moves")
-        # SetInput(u) through the delay line, then the plant over [t, t + Ts]
+        # SetInput(u) through the delay line, then the plant over [t, t + Ts];
+        # at the end of a segment's Integrate call: SetOffset and a new call
         self.sim.set_input(self.u_ctrl)
-        self.sim.integrate(t, t + self.Ts, REF_EPS, REF_EPS)
+        if self._sched and t >= self._sched[0][0] - 1e-9:
+            self.sim.set_offset(self._sched.pop(0)[1])
+            self.sim.restart(self.Ts)
+        else:
+            self.sim.integrate(t, t + self.Ts, REF_EPS, REF_EPS)
         self.k += 1
         return t, y
 

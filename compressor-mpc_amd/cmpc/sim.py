@@ -73,6 +73,16 @@ class PlantSimulator:
         check(self.lib.cmpc_sim_set_input(self._h, ctypes.c_void_p(u_control.data_ptr())),
               "cmpc_sim_set_input")
 
+    def set_offset(self, u_offset):
+        """SetOffset: u_offset (B, n_inputs) device tensor; the plant input
+        changes with the next set_input."""
+        check(self.lib.cmpc_sim_set_offset(self._h, ctypes.c_void_p(u_offset.data_ptr())),
+              "cmpc_sim_set_offset")
+
+    def restart(self, dt0: float = REF_TS):
+        """A new Integrate call: the carried step size starts again at dt0."""
+        check(self.lib.cmpc_sim_restart(self._h, dt0), "cmpc_sim_restart")
+
     def plant_input(self, u_control, out):
         """GetPlantInput without the delay line into out (B, n_inputs)."""
         check(self.lib.cmpc_sim_plant_input(self._h, ctypes.c_void_p(u_control.data_ptr()),

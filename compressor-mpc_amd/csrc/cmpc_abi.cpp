@@ -912,6 +912,24 @@ int cmpc_sim_set_input(cmpc_sim* m, const double* u_control) {
   return check_launch("sim input kernel");
 }
 
+int cmpc_sim_set_offset(cmpc_sim* m, const double* u_offset) {
+  if (!m || !u_offset) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  HIP_TRY(hipMemcpyAsync(m->u_offset, u_offset, sizeof(double) * (size_t)m->B * m->ni,
+                         hipMemcpyDeviceToDevice, m->stream));
+  return 0;
+}
+
+int cmpc_sim_restart(cmpc_sim* m, double dt0) {
+  if (!m) return fail("null simulator");
+  if (!(dt0 > 0)) return fail("cmpc_sim_restart: dt0 must be positive");
+  HIP_TRY(hipSetDevice(m->device));
+  std::vector<double> dts((size_t)m->B, dt0);
+  HIP_TRY(hipMemcpyAsync(m->dt, dts.data(), sizeof(double) * dts.size(), hipMemcpyHostToDevice, m->stream));
+  HIP_TRY(hipStreamSynchronize(m->stream));  // (host staging buffer)
+  return 0;
+}
+
 int cmpc_sim_plant_input(cmpc_sim* m, const double* u_control, double* u_full_out) {
   if (!m || !u_control || !u_full_out) return fail("null argument");
   HIP_TRY(hipSetDevice(m->device));

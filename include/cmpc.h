@@ -299,6 +299,16 @@ int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
  *                       Dormand-Prince with Boost odeint's semantics and the
  *                       reference's 2-norm error (:121-133); the step size
  *                       carries over between intervals as in integrate_const
+ *   cmpc_sim_set_offset SetOffset(u_offset) (simulation_system.h:64): the
+ *                       plant-input offset (B x n_inputs, device) that the next
+ *                       cmpc_sim_set_input adds the control inputs to; the
+ *                       current plant input is unchanged until then (the
+ *                       setup files' `simulation` segments, a step of an
+ *                       unmeasured input such as the discharge valve)
+ *   cmpc_sim_restart    a new Integrate call (simulation_system.h:108-116):
+ *                       integrate_const's controlled stepper starts again from
+ *                       the step size dt0 (the harness integrates each setup
+ *                       segment with its own call)
  *   cmpc_sim_output     GetOutput() (B x n_outputs, device)
  *   cmpc_sim_plant_input GetPlantInput(u_control) without the delay line (the
  *                       controller's linearisation input, nerve_center.h:139)
@@ -312,6 +322,8 @@ int cmpc_sim_destroy(cmpc_sim* sim);
 int cmpc_sim_set_stream(cmpc_sim* sim, void* hip_stream);
 int cmpc_sim_reset(cmpc_sim* sim, const double* x0, const double* u_offset, double dt0);
 int cmpc_sim_set_input(cmpc_sim* sim, const double* u_control);
+int cmpc_sim_set_offset(cmpc_sim* sim, const double* u_offset);
+int cmpc_sim_restart(cmpc_sim* sim, double dt0);
 int cmpc_sim_plant_input(cmpc_sim* sim, const double* u_control, double* u_full_out);
 int cmpc_sim_integrate(cmpc_sim* sim, double t, double t_end, double eps_abs, double eps_rel);
 int cmpc_sim_output(cmpc_sim* sim, double* y);

@@ -8,7 +8,8 @@ reads the reference).  The fixture holds data only:
   applied control input u (line 3), plant output y (line 4) — the record
   layout is SURVEY.md §4; all five runs agree to the printed 6 digits;
 * the run parameters of setup/setup-<cfg>-<plant>: n-iterations, yref, uwt,
-  ywt (one block per sub-controller for the distributed types), constraints.
+  ywt (one block per sub-controller for the distributed types), constraints,
+  simulation (segments: plant-input offset change, end time).
 
 The t=0 input is independent of the (missing) observer gain M, because the
 first ObserveAPosteriori adds M*(y - y_old - C*0) = 0
@@ -86,6 +87,7 @@ def main():
                 "constraints_upper": flat(setup["constraints-upper"]),
                 "rate_lower": flat(setup["constraints-rate-lower"]),
                 "rate_upper": flat(setup["constraints-rate-upper"]),
+                "simulation": flat(setup["simulation"]),
                 "x0": rec["x"], "u0": rec["u"], "y0": rec["y"],
             }
             out["configs"][f"{ctype}-{plant}"] = cfg

@@ -5,7 +5,7 @@ import os
 
 import numpy as np
 
-from cmpc.configs import SetupFile, reference_config
+from cmpc.configs import PLANT_N_INPUTS, SetupFile, reference_config
 from cmpc.problem import controller_arrays
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "step0.json")
@@ -26,8 +26,16 @@ def case(name, p=None):
     setup = SetupFile(n_iterations=g["n_iterations"], yref=g["yref"], uwt=g["uwt"], ywt=ywt,
                       constraints_lower=g["constraints_lower"],
                       constraints_upper=g["constraints_upper"],
-                      rate_lower=g["rate_lower"], rate_upper=g["rate_upper"])
+                      rate_lower=g["rate_lower"], rate_upper=g["rate_upper"],
+                      segments=segments(cfg, g["simulation"]))
     return cfg, setup, controller_arrays(cfg, setup), g
+
+
+def segments(cfg, flat):
+    """The `simulation` block as [(offset change (n_inputs), end time)]."""
+    n = PLANT_N_INPUTS[cfg.plant] + 1
+    assert len(flat) % n == 0, flat
+    return [(flat[i:i + n - 1], flat[i + n - 1]) for i in range(0, len(flat), n)]
 
 
 def step0_records(cfg, dims, layout, lin_record_fn, x0, u_full, y):

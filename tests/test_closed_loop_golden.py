@@ -1,0 +1,112 @@
+"""The whole recorded closed loop of every reference run (SURVEY.md §8(f)
+rows 2-3 around the hot path): plant simulation, observer, condensed-QP
+build, warm-started QP solves, K Jacobi iterations, input delay line and the
+setup files' 50 s plant-input step, for all 10 000 sampling instants (500 s)
+of the six configurations, against the reference's own records
+(results/<plant>/run1/<cfg>.dat -> tests/golden/traj_long.npz, made by
+tests/golden/make_traj_long.py).
+
+Two facts of the missing harness (common-simulation.inc) are identified from
+the records, not assumed:
+  * the observer gain M = [0; I] (cmpc.reference_observer_gain;
+    tools/fit_observer_gain.py: every other gain [0; g I] changes u(t) in the
+    first steps);
+  * each `simulation` segment is its own Integrate call, so the instant at a
+    segment boundary is observed twice (cmpc/driver.py docstring; the
+    records printed at 50 and 50.05 s hold the same plant state).
+With both, u(t) and y(t) equal the records to all 6 printed digits at every
+instant.  Comparison: string equality of %.6g; |v| < 1e-12 counts as 0 (the
+parallel plant's y[2] is a difference of two identical compressors' values,
+0 up to one ulp of cancellation, which the reference prints as 0 or
+2.22045e-16 depending on rounding order)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import golden_cases as GC
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LONG = os.path.join(HERE, "golden", "traj_long.npz")
+TRAJ = {"cent-par": "par_centralized", "coop-par": "par_coop9", "ncoop-par": "par_ncoop9",
+        "cent-ser": "ser_centralized", "coop-ser": "ser_coop9", "ncoop-ser": "ser_ncoop9"}
+
+
+def six(a):
+    a = np.asarray(a, dtype=np.float64)
+    return np.array([0.0 if abs(v) < 1e-12 else float("%.6g" % v) for v in a.ravel()]).reshape(a.shape)
+
+
+# ---- CPU: the fixture -----------------------------------------------------------
+
+@pytest.mark.parametrize("name", list(TRAJ))
+def test_long_fixture_agrees_with_first_records(name):
+    """traj_long.npz (float32 of the printed values) holds the same first 160
+    records as traj_<name>.json (parsed text) and 10 000 records in all."""
+    g = np.load(LONG)
+    u, y = g[TRAJ[name] + "_u"], g[TRAJ[name] + "_y"]
+    assert u.shape == (10000, 4) and y.shape == (10000, 4)
+    recs = json.load(open(os.path.join(HERE, "golden", f"traj_{TRAJ[name]}.json")))["records"]
+    for k, r in enumerate(recs):
+        assert ["%.6g" % v for v in u[k]] == ["%.6g" % v for v in r["u"]]
+        assert ["%.6g" % v for v in y[k]] == ["%.6g" % v for v in r["y"]]
+
+
+def test_reference_observer_gain_shape():
+    import cmpc
+    from cmpc._abi import CmpcDims
+    for name in TRAJ:
+        cfg, _, _, _ = GC.case(name)
+        M = cmpc.reference_observer_gain(cfg)
+        L = cmpc.layout_of(CmpcDims.from_config(cfg, 1))
+        assert M.shape == (L.nobs, 4)
+        assert np.array_equal(M[cfg.ns:], np.eye(4)) and not M[:cfg.ns].any()
+
+
+# ---- GPU: the device closed loop against the records ----------------------------
+
+@pytest.fixture(autouse=True)
+def _torch_first(request):
+    if request.node.get_closest_marker("gpu"):
+        import torch
+        torch.cuda.init()
+    yield
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(TRAJ))
+def test_gpu_closed_loop_reproduces_reference_run(name):
+    """B = 3 identical scenarios (batched, bit-identical to each other) for the
+    10 000 recorded instants."""
+    import torch
+    import cmpc
+    from cmpc.driver import ClosedLoop
+    cfg, setup, arr, g = GC.case(name)
+    gold = np.load(LONG)
+    ur = gold[TRAJ[name] + "_u"].astype(np.float64)
+    yr = gold[TRAJ[name] + "_y"].astype(np.float64)
+    n, B = len(ur), 3
+    x0, u_def = cmpc.plant_default(cfg.plant)
+    M = cmpc.reference_observer_gain(cfg)
+    loop = ClosedLoop(cfg, arr, [M] * cfg.S, np.tile(x0, (B, 1)), np.tile(u_def, (B, 1)), g["n_iterations"])
+    ub = torch.zeros(n, B, 4, dtype=torch.float64, device="cuda")
+    yb = torch.zeros(n, B, 4, dtype=torch.float64, device="cuda")
+    try:
+        loop.set_segments(setup.segments, u_def)
+        loop.initialize()
+        for k in range(n):
+            _, y = loop.step()
+            ub[k].copy_(loop.u_ctrl)
+            yb[k].copy_(y)
+        x, _, _, st = loop.sim.download()
+    finally:
+        loop.close()
+    assert not st.any()
+    u, y = ub.cpu().numpy(), yb.cpu().numpy()
+    for b in range(1, B):
+        assert np.array_equal(u[:, b], u[:, 0]) and np.array_equal(y[:, b], y[:, 0])
+    bad_u = np.flatnonzero(np.any(six(u[:, 0]) != six(ur), axis=1))
+    bad_y = np.flatnonzero(np.any(six(y[:, 0]) != six(yr), axis=1))
+    assert bad_u.size == 0, ("u differs at records", bad_u[:5], u[bad_u[:2], 0], ur[bad_u[:2]])
+    assert bad_y.size == 0, ("y differs at records", bad_y[:5], y[bad_y[:2], 0], yr[bad_y[:2]])

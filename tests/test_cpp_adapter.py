@@ -32,6 +32,9 @@ def write_setup(path, g, ny, S):
     blk = ny * ny
     yw = g["ywt"]
     blocks = [yw[i * blk:(i + 1) * blk] for i in range(len(yw) // blk)]
+    n = (9 if g["plant"] == "parallel" else 8) + 1
+    sim = g["simulation"]
+    segs = [(sim[i:i + n - 1], sim[i + n - 1]) for i in range(0, len(sim), n)]
     parts = [
         ("n-iterations", str(g["n_iterations"])),
         ("n-timing-iterations", str(g["n_iterations"])),
@@ -44,6 +47,7 @@ def write_setup(path, g, ny, S):
         ("constraints-upper", "\t".join("%g" % v for v in g["constraints_upper"])),
         ("constraints-rate-lower", "\t".join("%g" % v for v in g["rate_lower"])),
         ("constraints-rate-upper", "\t".join("%g" % v for v in g["rate_upper"])),
+        ("simulation", "\n\n".join(" ".join("%g" % v for v in d) + "\n%g" % te for d, te in segs)),
     ]
     with open(path, "w") as fh:
         for k, v in parts:
@@ -74,6 +78,7 @@ def test_setup_writer_roundtrip(tmp_path):
     assert back.uwt == g["uwt"]
     assert back.ywt[0] == setup.ywt[0] and back.ywt[1] == setup.ywt[1]
     assert back.rate_upper == g["rate_upper"]
+    assert back.segments == setup.segments
 
 
 @pytest.mark.gpu

@@ -74,3 +74,4 @@ def test_product_reference_setups_match_setup_files(name):
     assert mine.constraints_lower == g["constraints_lower"]
     assert mine.constraints_upper == g["constraints_upper"]
     assert mine.rate_lower == g["rate_lower"] and mine.rate_upper == g["rate_upper"]
+    assert mine.segments == setup.segments and len(mine.segments) == 2
