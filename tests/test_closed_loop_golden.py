@@ -53,6 +53,32 @@ def test_long_fixture_agrees_with_first_records(name):
         assert ["%.6g" % v for v in y[k]] == ["%.6g" % v for v in r["y"]]
 
 
+@pytest.mark.parametrize("name,n", [(k, 2000) for k in TRAJ] + [("coop-par", 10000)],
+                         ids=[f"{k}-2000" for k in TRAJ] + ["coop-par-10000"])
+def test_oracle_closed_loop_reproduces_reference_run(name, n):
+    """The oracle's closed loop (tests/oracle_loop.py: or_observe_post,
+    or_lin_record, or_step, or_observe_prior, or_sim_interval) with the same
+    two identified harness facts reproduces the records too: the first 2000
+    instants (100 s, across the 50 s input step) of every run, and the whole
+    500 s of the cooperative parallel run."""
+    import cmpc
+    from oracle_loop import OracleClosedLoop
+    cfg, setup, arr, g = GC.case(name)
+    gold = np.load(LONG)
+    ur = gold[TRAJ[name] + "_u"].astype(np.float64)
+    yr = gold[TRAJ[name] + "_y"].astype(np.float64)
+    loop = OracleClosedLoop(cfg, arr, [cmpc.reference_observer_gain(cfg)] * cfg.S, g["n_iterations"],
+                            setup.segments)
+    u, y = np.zeros((n, 4)), np.zeros((n, 4))
+    for k in range(n):
+        y[k] = loop.step()
+        u[k] = loop.u_ctrl
+    bad_u = np.flatnonzero(np.any(six(u) != six(ur[:n]), axis=1))
+    bad_y = np.flatnonzero(np.any(six(y) != six(yr[:n]), axis=1))
+    assert bad_u.size == 0, ("u differs at records", bad_u[:5])
+    assert bad_y.size == 0, ("y differs at records", bad_y[:5])
+
+
 def test_reference_observer_gain_shape():
     import cmpc
     from cmpc._abi import CmpcDims
