@@ -105,13 +105,16 @@ class ClosedLoop:
 
     def set_segments(self, segments, u_default):
         """The setup file's `simulation` segments ([(offset change, end time)],
-        SetupFile.segments) over the plant's default input u_default: segment 0's
+        SetupFile.segments) over the plant's default input u_default (offset
+        changes and u_default may be per scenario, (B, n_inputs)): segment 0's
         offset is the initial one (call before initialize); segment i's is set
         after the last instant of segment i-1 (its end time), which no
         integration follows (module docstring)."""
         torch = self.torch
         u_default = np.asarray(u_default, dtype=np.float64)
-        offs = [np.tile(u_default + np.asarray(d, dtype=np.float64), (self.B, 1)) for d, _ in segments]
+        # per-scenario defaults and changes broadcast: (n_inputs,) or (B, n_inputs)
+        offs = [np.array(np.broadcast_to(u_default + np.asarray(d, dtype=np.float64), (self.B, u_default.shape[-1])))
+                for d, _ in segments]
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
         self.u_offset = t(offs[0])
         self._sched = [(float(segments[i - 1][1]), t(offs[i])) for i in range(1, len(segments))]

@@ -47,6 +47,7 @@ constexpr double dc1 = c1 - 5179.0 / 57600.0, dc3 = c3 - 7571.0 / 16695.0,
                  dc4 = c4 - 393.0 / 640.0, dc5 = c5 - -92097.0 / 339200.0,
                  dc6 = c6 - 187.0 / 2100.0, dc7 = -1.0 / 40.0;
 constexpr double kEps = 2.220446049250313e-16;  // numeric_limits<double>::epsilon()
+constexpr int kMaxSteps = 500;                  // odeint max_step_checker default
 
 template <int PLANT>
 __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
@@ -62,9 +63,15 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
   double dt = P.dt[b];
   double t = P.t;
   const double t_end = P.t_end;
-  int status = 0;
+  int status = 0, steps = 0;
   F::f(P.p_in, P.p_out, x, u, k1);  // a fresh stepper per interval: initialize
   while (t_end - t > kEps) {
+    // odeint's max_step_checker: at most 500 steps between two observer calls
+    // (every lane leaves the loop even when the step size collapses)
+    if (++steps > kMaxSteps) {
+      status = 2;
+      break;
+    }
     if ((t + dt) - t_end > kEps) dt = t_end - t;
     int fails = 0;
     for (;;) {

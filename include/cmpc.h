@@ -313,7 +313,9 @@ int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
  *   cmpc_sim_plant_input GetPlantInput(u_control) without the delay line (the
  *                       controller's linearisation input, nerve_center.h:139)
  * Device arrays: cmpc_sim_state (x), cmpc_sim_input (plant input u_),
- * cmpc_sim_step_size (dt), cmpc_sim_status (1 = step-size control failed). */
+ * cmpc_sim_step_size (dt), cmpc_sim_status (1 = step-size control failed:
+ * 500 rejected tries of one step; 2 = more than 500 steps in one interval,
+ * odeint's max_step_checker; the scenario's state stays where it stopped). */
 typedef struct cmpc_sim cmpc_sim;
 int cmpc_sim_create(cmpc_sim** sim, int plant, int B, int device, double p_in, double p_out,
                     int n_control, const int32_t* delays /* n_control, control order */,

@@ -121,8 +121,8 @@ int or_plant_derivative(int plant, double p_in, double p_out, const double* x,
                         const double* u, double* dx);
 /* One observation interval [t, t_end] of SimulationSystem::Integrate
  * (controlled Dormand-Prince, odeint semantics, see or_sim.c); x in/out,
- * dt in/out (carried between intervals).  Returns accepted steps, <0 on
- * failure (500 rejected tries). */
+ * dt in/out (carried between intervals).  Returns accepted steps; -1 after
+ * 500 rejected tries of one step, -2 after 500 steps in the interval. */
 int or_sim_interval(int plant, double p_in, double p_out, const double* u_full, double* x,
                     double t, double t_end, double* dt_io, double eps_abs, double eps_rel);
 /* TimeDelay (time_delay.h:26-58): ring = sum(delays) doubles, cur = n_inputs. */

@@ -21,6 +21,8 @@
  *     size dt carried by reference from interval to interval;
  *   - integrate_adaptive: while t_end - t > eps: clip dt to t_end - t when
  *     t + dt - t_end > eps; try_step until success (500 failures throw);
+ *     integrate_const's max_step_checker throws after 500 steps between two
+ *     observer calls (here: return -2, the device sets status 2);
  *   - try_step: one Dormand-Prince 5(4) step; err = ||e_i / (eps_abs +
  *     eps_rel (|x_i| + dt |dxdt_i|))||; err > 1: reject, dt *= max(0.9
  *     err^(-1/3), 0.2); else accept, t += dt and, if err < 0.5,
@@ -92,6 +94,10 @@ int or_sim_interval(int plant, double p_in, double p_out, const double* u_full, 
   or_plant_derivative(plant, p_in, p_out, x, u_full, dxdt); /* fresh stepper: initialize */
   int count = 0;
   while (t_end - t > DBL_EPSILON) {
+    if (count >= 500) { /* max_step_checker: 500 steps between observer calls */
+      *dt_io = dt;
+      return -2;
+    }
     if ((t + dt) - t_end > DBL_EPSILON) dt = t_end - t;
     int fails = 0;
     for (;;) {

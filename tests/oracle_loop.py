@@ -21,12 +21,12 @@ TS = 0.05
 
 
 class OracleClosedLoop:
-    def __init__(self, cfg, arrays, M, K, segments=None, B=1):
-        assert B == 1
+    def __init__(self, cfg, arrays, M, K, segments=None, x0=None):
         self.cfg, self.arr, self.M, self.K = cfg, arrays, M, K
         self.dims = CmpcDims.from_config(cfg, 1)
         self.L = O.layout(self.dims)
-        x0, u_def = O.plant_default(cfg.plant)
+        xd, u_def = O.plant_default(cfg.plant)
+        x0 = xd if x0 is None else np.asarray(x0, dtype=np.float64)
         segs = segments or [([0.0] * len(u_def), float("inf"))]
         offs = [u_def + np.asarray(d, dtype=np.float64) for d, _ in segs]
         self.u_off = offs[0].copy()                       # the controller's (NerveCenter::Initialize)

@@ -71,6 +71,29 @@ def test_oracle_time_delay_ring():
     assert np.array_equal(outs[:, 3], [0, 0, 30, 31, 32, 33, 34, 35])
 
 
+def _unstable_serial():
+    """Serial plant with its input 6 stepped by -0.3 (0.393 -> 0.093), no
+    control: the step size collapses within 10 intervals."""
+    x0, u0 = O.plant_default(1)
+    u = u0.copy()
+    u[6] -= 0.3
+    return x0, u
+
+
+def test_oracle_sim_step_bound():
+    """odeint's max_step_checker: more than 500 steps between two observer
+    calls end the interval (or_sim_interval returns -2) instead of looping
+    while the step size collapses."""
+    x0, u = _unstable_serial()
+    sim = O.PlantSim(1, x0, u)
+    rcs = []
+    for k in range(12):
+        sim.set_input(np.zeros(4))
+        rcs.append(sim.L.or_sim_interval(1, 1.0, 1.0, O.dptr(sim.u_full), O.dptr(sim.x), k * TS,
+                                         k * TS + TS, O.dptr(sim.dt), 1e-6, 1e-6))
+    assert all(0 < r <= 500 for r in rcs[:10]) and rcs[10] == -2, rcs
+
+
 # ---- GPU ----------------------------------------------------------------------
 
 @pytest.fixture(autouse=True)
@@ -137,6 +160,29 @@ def test_gpu_sim_matches_oracle(plant):
     np.testing.assert_array_equal(uf, np.stack([s.u_full for s in sims]))
     np.testing.assert_allclose(x, ox, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(dt, np.array([s.dt[0] for s in sims]), rtol=1e-10)
+
+
+@pytest.mark.gpu
+def test_gpu_sim_step_bound():
+    """The device integrator stops a scenario whose step size collapses after
+    500 steps in the interval (status 2), like the oracle, and its neighbour
+    in the batch is unaffected (status 0, state equal to the oracle's)."""
+    import torch
+    from cmpc.sim import PlantSimulator
+    x0, u_bad = _unstable_serial()
+    _, u0 = O.plant_default(1)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    good = O.PlantSim(1, x0, u0)
+    with PlantSimulator(1, 2) as sim:
+        sim.reset(dev(np.stack([x0, x0])), dev(np.stack([u0, u_bad])), TS)
+        for k in range(11):
+            sim.set_input(dev(np.zeros((2, 4))))
+            sim.integrate(k * TS, k * TS + TS)
+            good.set_input(np.zeros(4))
+            good.integrate(k * TS, k * TS + TS)
+            x, _, _, st = sim.download()
+            assert st[0] == 0 and st[1] == (2 if k == 10 else 0), (k, st)
+        np.testing.assert_allclose(x[0], good.x, rtol=1e-12)
 
 
 # ---- the closed-loop driver (cmpc/driver.py) -----------------------------------
