@@ -313,12 +313,9 @@ def main():
         # (SURVEY §8(f) row 2): a posteriori update + linearisation at each
         # slot's x_hat, build, K iterations, a priori update + u_old += du
         try:
-            # the reference's gain M is unknown (missing harness include): a
-            # disturbance-only gain [0; 0.5 I] (offset-free MPC convention);
-            # a random gain is an unstable observer (tools/closed_loop_observer.py)
-            L0 = ctx.layout
-            Mg = np.zeros((L0.nobs, ys.shape[1]))
-            Mg[cfg.ns:cfg.ns + cfg.ndist, :cfg.ndist] = 0.5 * np.eye(cfg.ndist)
+            # the reference runs' gain M = [0; I], identified from their records
+            # (cmpc.reference_observer_gain, tests/test_closed_loop_golden.py)
+            Mg = cmpc.reference_observer_gain(cfg, ys.shape[1])
             for s_ in range(S):
                 ctx.set_observer(s_, Mg)
             warm()
@@ -367,7 +364,7 @@ def main():
                 "qp_solves_per_s": B * S * K / t_full,
                 "note": "observe a posteriori + per-QP linearisation at x_hat (records), build, "
                         "K iterations, observe a priori + u_old update; measured y held fixed, "
-                        f"disturbance-only observer gain [0; 0.5 I], {reps} consecutive steps"}
+                        f"the reference runs' observer gain [0; I], {reps} consecutive steps"}
         except Exception as e:
             log(f"observer closed-loop variant failed: {e}")
     except Exception as e:  # reported, never required

@@ -7,11 +7,12 @@ written in the reference's results/*.dat format.
 usage: run_closed_loop.py <par|ser> <cent|coop|ncoop> [--setup FILE] [--steps N]
                           [--batch B] [--p P] [--out FILE] [--gain G] [--perturb E]
 
-The observer gain of the reference harness is unknown (its
-common-simulation.inc is missing); --gain G uses the disturbance-only gain
-[0; G I] (offset-free MPC convention).  Record 0 and the plant state of
-record 1 do not depend on it and equal the reference's results (tests/
-test_sim.py); later records do.
+The observer gain defaults to the reference runs' M = [0; I]
+(cmpc.reference_observer_gain, identified from their records); --gain G uses
+[0; G I] instead.  The setup's `simulation` segments step the plant-input
+offset (ClosedLoop.set_segments).  With the defaults and --steps 10000 the
+written records equal the reference's results/<plant>/run1/<cfg>.dat to the
+printed digits except the wall-time line (tests/test_closed_loop_golden.py).
 """
 import argparse
 import json
@@ -34,7 +35,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--p", type=int, default=100)
     ap.add_argument("--out", default=None, help=".dat output for scenario 0")
-    ap.add_argument("--gain", type=float, default=0.5)
+    ap.add_argument("--gain", type=float, default=None)
     ap.add_argument("--perturb", type=float, default=0.0, help="relative perturbation of x0 per scenario")
     args = ap.parse_args()
     import torch
@@ -49,9 +50,10 @@ def main():
     arr = cmpc.controller_arrays(cfg, setup)
     L = cmpc.layout_of(CmpcDims.from_config(cfg, 1))
     x0, u0 = cmpc.plant_default(cfg.plant)
-    no = 4
-    Mg = np.zeros((L.nobs, no))
-    Mg[cfg.ns:cfg.ns + cfg.ndist, :cfg.ndist] = args.gain * np.eye(cfg.ndist)
+    Mg = cmpc.reference_observer_gain(cfg)
+    if args.gain is not None:
+        Mg = Mg * args.gain
+    assert Mg.shape[0] == L.nobs
     B = args.batch
     rng = np.random.default_rng(0)
     xs = np.tile(x0, (B, 1))
@@ -60,6 +62,8 @@ def main():
     loop = ClosedLoop(cfg, arr, [Mg] * cfg.S, xs, np.tile(u0, (B, 1)), setup.n_iterations)
     writer = DatWriter(args.out) if args.out else None
     try:
+        if setup.segments:
+            loop.set_segments(setup.segments, u0)
         loop.initialize()
         t0 = time.perf_counter()
         per_step = loop.run(args.steps, writer)
@@ -76,7 +80,7 @@ def main():
         "scenario_steps_per_s": B / per_step, "wall_s": wall,
         "qp_status_ok_fraction_last_step": float((st == 0).mean()),
         "plant_step_failures": int(sst.sum()),
-        "observer_gain": f"[0; {args.gain} I] (disturbance-only)"}))
+        "observer_gain": f"[0; {1.0 if args.gain is None else args.gain} I]"}))
 
 
 if __name__ == "__main__":
