@@ -96,7 +96,8 @@ EXPORTS = (
     "cmpc_sim_create", "cmpc_sim_destroy", "cmpc_sim_set_stream", "cmpc_sim_reset",
     "cmpc_sim_set_input", "cmpc_sim_set_offset", "cmpc_sim_restart", "cmpc_sim_plant_input", "cmpc_sim_integrate", "cmpc_sim_output",
     "cmpc_sim_synchronize", "cmpc_sim_state", "cmpc_sim_input", "cmpc_sim_step_size",
-    "cmpc_sim_status", "cmpc_accumulate_moves", "cmpc_sim_download",
+    "cmpc_sim_status", "cmpc_accumulate_moves", "cmpc_sim_download", "cmpc_sim_reset_host",
+    "cmpc_sim_set_input_host", "cmpc_sim_set_offset_host", "cmpc_sim_output_host",
 )
 
 _lib = None

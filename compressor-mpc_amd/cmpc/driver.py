@@ -132,13 +132,17 @@ class ClosedLoop:
         self.ctx.build()
         self.ctx.init_warmstart()
         self.k = 0
+        self.t_seg, self.seg_step = 0.0, 0   # integrate_const's start time and step count
 
     def step(self):
         """One sampling instant: returns (t, y) of the instant; the plant has
         advanced to the next one."""
         from ._abi import check, iptr
         torch = self.torch
-        t = 0.0 + self.k * self.Ts   # integrate_const: t0 + step * dt
+        t = 0.0 + self.k * self.Ts   # the record's label (record count)
+        # integrate_const's own time: start_time + step * dt of the current
+        # Integrate call; its interval ends at time + dt
+        t_int = self.t_seg + self.seg_step * self.Ts
         y = self.sim.output()
         # GetNextInputWithTiming(y): linearisation input GetPlantInput(u_old_,
         # u_offset_) with the controller's own offset (fixed at Initialize; the
@@ -154,11 +158,14 @@ class ClosedLoop:
         # SetInput(u) through the delay line, then the plant over [t, t + Ts];
         # at the end of a segment's Integrate call: SetOffset and a new call
         self.sim.set_input(self.u_ctrl)
-        if self._sched and t >= self._sched[0][0] - 1e-9:
+        if self._sched and t_int >= self._sched[0][0] - 1e-9:
+            self.t_seg = self._sched[0][0]
+            self.seg_step = 0
             self.sim.set_offset(self._sched.pop(0)[1])
             self.sim.restart(self.Ts)
         else:
-            self.sim.integrate(t, t + self.Ts, REF_EPS, REF_EPS)
+            self.sim.integrate(t_int, t_int + self.Ts, REF_EPS, REF_EPS)
+            self.seg_step += 1
         self.k += 1
         return t, y
 

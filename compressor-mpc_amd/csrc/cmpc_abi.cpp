@@ -780,7 +780,7 @@ struct cmpc_sim {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   double *x = nullptr, *dt = nullptr, *u_full = nullptr, *u_offset = nullptr, *ring = nullptr,
-         *scratch = nullptr;
+         *scratch = nullptr, *stage = nullptr;  // stage: host-variant staging (B x max(ns, ni, no, nc))
   int32_t *cur = nullptr, *status = nullptr;
 };
 
@@ -810,7 +810,7 @@ int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, d
   if (m->ring_len == 0) m->ring_len = 1;
   auto bail = [&](hipError_t e) {
     (void)e;
-    void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->cur, m->status};
+    void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->cur, m->status};
     for (void* b : bufs)
       if (b) (void)hipFree(b);
     delete m;
@@ -827,6 +827,8 @@ int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, d
       (e = hipMalloc(&m->u_offset, sizeof(double) * Bz * ni)) != hipSuccess ||
       (e = hipMalloc(&m->ring, sizeof(double) * Bz * m->ring_len)) != hipSuccess ||
       (e = hipMalloc(&m->scratch, sizeof(double) * Bz * (ni > n_control ? ni : n_control))) != hipSuccess ||
+      (e = hipMalloc(&m->stage, sizeof(double) * Bz * 2 * std::max(std::max(ns, ni), std::max(no, n_control)))) !=
+          hipSuccess ||
       (e = hipMalloc(&m->cur, sizeof(int32_t) * Bz * n_control)) != hipSuccess ||
       (e = hipMalloc(&m->status, sizeof(int32_t) * Bz)) != hipSuccess)
     return bail(e);
@@ -838,7 +840,7 @@ int cmpc_sim_destroy(cmpc_sim* m) {
   if (!m) return 0;
   (void)hipSetDevice(m->device);
   if (m->stream) (void)hipStreamSynchronize(m->stream);
-  void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->cur, m->status};
+  void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->cur, m->status};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (m->own_stream && m->stream) (void)hipStreamDestroy(m->stream);
@@ -979,6 +981,45 @@ int cmpc_sim_download(cmpc_sim* m, double* x, double* u_full, double* dt, int32_
     HIP_TRY(hipMemcpyAsync(status, m->status, sizeof(int32_t) * Bz, hipMemcpyDeviceToHost, m->stream));
   HIP_TRY(hipStreamSynchronize(m->stream));
   return 0;
+}
+
+// Host-array variants: stage through the simulator's device buffer; each
+// returns once the call's work is done (the host arrays are free again).
+static int sim_stage(cmpc_sim* m, const double* h0, size_t n0, const double* h1, size_t n1) {
+  HIP_TRY(hipSetDevice(m->device));
+  const size_t half = (size_t)m->B * std::max(std::max(m->ns, m->ni), std::max(m->no, m->nc));
+  if (n0) HIP_TRY(hipMemcpyAsync(m->stage, h0, sizeof(double) * n0, hipMemcpyHostToDevice, m->stream));
+  if (n1) HIP_TRY(hipMemcpyAsync(m->stage + half, h1, sizeof(double) * n1, hipMemcpyHostToDevice, m->stream));
+  return 0;
+}
+
+int cmpc_sim_reset_host(cmpc_sim* m, const double* x0, const double* u_offset, double dt0) {
+  if (!m || !x0 || !u_offset) return fail("null argument");
+  const size_t half = (size_t)m->B * std::max(std::max(m->ns, m->ni), std::max(m->no, m->nc));
+  if (sim_stage(m, x0, (size_t)m->B * m->ns, u_offset, (size_t)m->B * m->ni)) return -1;
+  return cmpc_sim_reset(m, m->stage, m->stage + half, dt0);  // (synchronises)
+}
+
+int cmpc_sim_set_input_host(cmpc_sim* m, const double* u_control) {
+  if (!m || !u_control) return fail("null argument");
+  if (sim_stage(m, u_control, (size_t)m->B * m->nc, nullptr, 0)) return -1;
+  if (cmpc_sim_set_input(m, m->stage)) return -1;
+  return cmpc_sim_synchronize(m);
+}
+
+int cmpc_sim_set_offset_host(cmpc_sim* m, const double* u_offset) {
+  if (!m || !u_offset) return fail("null argument");
+  if (sim_stage(m, u_offset, (size_t)m->B * m->ni, nullptr, 0)) return -1;
+  if (cmpc_sim_set_offset(m, m->stage)) return -1;
+  return cmpc_sim_synchronize(m);
+}
+
+int cmpc_sim_output_host(cmpc_sim* m, double* y) {
+  if (!m || !y) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  if (cmpc_sim_output(m, m->stage)) return -1;
+  HIP_TRY(hipMemcpyAsync(y, m->stage, sizeof(double) * (size_t)m->B * m->no, hipMemcpyDeviceToHost, m->stream));
+  return cmpc_sim_synchronize(m);
 }
 
 double* cmpc_sim_state(cmpc_sim* m) { return m ? m->x : nullptr; }

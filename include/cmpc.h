@@ -330,6 +330,12 @@ int cmpc_sim_plant_input(cmpc_sim* sim, const double* u_control, double* u_full_
 int cmpc_sim_integrate(cmpc_sim* sim, double t, double t_end, double eps_abs, double eps_rel);
 int cmpc_sim_output(cmpc_sim* sim, double* y);
 int cmpc_sim_synchronize(cmpc_sim* sim);
+/* Host-array variants of reset / set_input / set_offset / output (staged
+ * through the simulator's own device buffer; each returns once done). */
+int cmpc_sim_reset_host(cmpc_sim* sim, const double* x0, const double* u_offset, double dt0);
+int cmpc_sim_set_input_host(cmpc_sim* sim, const double* u_control);
+int cmpc_sim_set_offset_host(cmpc_sim* sim, const double* u_offset);
+int cmpc_sim_output_host(cmpc_sim* sim, double* y);
 /* Host copies (any pointer may be NULL): x B x ns, plant input B x n_inputs,
  * step size B, status B. */
 int cmpc_sim_download(cmpc_sim* sim, double* x, double* u_full, double* dt, int32_t* status);

@@ -122,6 +122,10 @@ struct ControllerSpec {
 struct SetupFile {
   int n_iterations = 1, n_timing_iterations = 1;
   std::vector<double> yref, uwt, ywt, lower, upper, rate_lower, rate_upper;
+  // `simulation`: segments of n_inputs plant-input offset changes (from the
+  // default input) and an end time, in file order
+  std::vector<double> simulation;
+  std::string folder_name, output_filename;
 
   static SetupFile Read(const std::string& path) {
     std::ifstream in(path);
@@ -146,10 +150,13 @@ struct SetupFile {
         dst = key == "yref" ? &s.yref : key == "uwt" ? &s.uwt : key == "ywt" ? &s.ywt
             : key == "constraints-lower" ? &s.lower : key == "constraints-upper" ? &s.upper
             : key == "constraints-rate-lower" ? &s.rate_lower
-            : key == "constraints-rate-upper" ? &s.rate_upper : &scratch;
+            : key == "constraints-rate-upper" ? &s.rate_upper
+            : key == "simulation" ? &s.simulation : &scratch;
         continue;
       }
       if (key.empty()) throw Error("Error reading setup file at line: " + line);
+      if (key == "folder-name") s.folder_name = tok;
+      if (key == "output-filename") s.output_filename = tok;
       if (key == "folder-name" || key == "output-filename") continue;
       std::istringstream vs(line);
       double v;
@@ -163,6 +170,17 @@ struct SetupFile {
     return s;
   }
 };
+
+// The observer gain M of the reference's runs, (ns + ndist) x n_outputs
+// row-major: M = [0; I], the innovation corrects the disturbance states at
+// unit gain.  The reference harness sets M in its missing
+// common-simulation.inc; this one reproduces every recorded run
+// (tests/test_closed_loop_golden.py).
+inline std::vector<double> ReferenceObserverGain(const ControllerSpec& spec) {
+  std::vector<double> M(static_cast<size_t>(spec.ns + spec.ndist) * spec.n_outputs, 0.0);
+  for (int o = 0; o < spec.ndist && o < spec.n_outputs; ++o) M[(spec.ns + o) * spec.n_outputs + o] = 1.0;
+  return M;
+}
 
 // InputConstraints<nu> (include/input_constraints.h:12-26): bounds on one
 // sub-controller's own inputs, nu values each.  As in the reference the rate

@@ -43,10 +43,11 @@ class OracleClosedLoop:
         self.ws = np.zeros(nq, np.uint32)
         self.u_ctrl = np.zeros(cfg.nu_tot)
         self.k = 0
+        self.t_seg, self.seg_step = 0.0, 0   # integrate_const's start time and step count
 
     def step(self):
         cfg, S = self.cfg, self.cfg.S
-        t = self.k * TS
+        t = self.t_seg + self.seg_step * TS
         y = O.plant_output(cfg.plant, self.sim.x)
         u_lin = self.u_off.copy()
         u_lin[list(CTRL)] += self.u_ctrl
@@ -66,9 +67,11 @@ class OracleClosedLoop:
             self.u_ctrl[own] += du[q, :cfg.nu]
         self.sim.set_input(self.u_ctrl)
         if self.sched and t >= self.sched[0][0] - 1e-9:
+            self.t_seg, self.seg_step = self.sched[0][0], 0
             self.sim.u_offset[:] = self.sched.pop(0)[1]
             self.sim.dt[0] = TS
         else:
             self.sim.integrate(t, t + TS)
+            self.seg_step += 1
         self.k += 1
         return y

@@ -143,7 +143,12 @@ def test_gpu_closed_loop_reproduces_reference_run(name):
 def test_gpu_closed_loop_scenarios_match_oracle(name):
     """B = 6 different scenarios in one batch (perturbed initial states,
     each its own size of the plant-input step at 10 s), 600 instants, against
-    one oracle closed loop per scenario, to the 6 printed digits."""
+    one oracle closed loop per scenario: u and y within rtol 2e-6 (the 6
+    printed digits) and atol 1e-10.  The absolute floor is for values that
+    are cancellation residues (the parallel plant's y[2], ~1e-9 when the two
+    compressors start apart): the build's summation order differs from the
+    oracle's (rtol 1e-9 on H, f), which moves such residues in their 6th
+    digit."""
     import torch
     import cmpc
     from cmpc.driver import ClosedLoop
@@ -182,5 +187,5 @@ def test_gpu_closed_loop_scenarios_match_oracle(name):
                                [(np.zeros(len(u_def)), 10.0), (deltas[b], 1e9)], x0=xs[b])
         for k in range(n):
             yo = ora.step()
-            assert np.array_equal(six(u[k, b]), six(ora.u_ctrl)), (b, k, u[k, b], ora.u_ctrl)
-            assert np.array_equal(six(y[k, b]), six(yo)), (b, k, y[k, b], yo)
+            np.testing.assert_allclose(u[k, b], ora.u_ctrl, rtol=2e-6, atol=1e-10, err_msg=f"u {b} {k}")
+            np.testing.assert_allclose(y[k, b], yo, rtol=2e-6, atol=1e-10, err_msg=f"y {b} {k}")

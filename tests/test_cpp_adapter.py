@@ -3,8 +3,11 @@ API over the C ABI — driven like the reference's tests/*-with-timing.cc
 harnesses: a setup file in the reference's format, SetWeights /
 SetOutputReference / constraints, Initialize, GetNextInputWithTiming.
 
-CPU: the driver builds and fails loudly (no CPU fallback) without a device.
-GPU: u(t = 0) matches the reference's own step-0 records (6 digits).
+CPU: the drivers build and fail loudly (no CPU fallback) without a device.
+GPU: u(t = 0) matches the reference's own step-0 records (6 digits); the
+closed-loop timing executable (tests/cpp/with_timing.cpp: NerveCenter +
+SimulationSystem, the replacement of the missing common-simulation.inc)
+writes the reference's recorded runs.
 """
 import os
 import subprocess
@@ -15,11 +18,12 @@ import golden_cases as GC
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DRIVER = os.path.join(HERE, "cpp", "nerve_center_step0")
+HARNESS = os.path.join(HERE, "cpp", "with_timing")
 
 
 def _build():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "cpp"), "nerve_center_step0"])
-    assert os.path.exists(DRIVER)
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "cpp"), "nerve_center_step0", "with_timing"])
+    assert os.path.exists(DRIVER) and os.path.exists(HARNESS)
 
 
 def _mat(vals, n):
@@ -67,6 +71,18 @@ def test_driver_builds_and_fails_loudly_without_device(tmp_path):
     assert "error: cmpc_create" in r.stderr
 
 
+def test_harness_builds_and_fails_loudly_without_device(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    _build()
+    cfg, _, _, g = GC.case("coop-par")
+    setup = tmp_path / "setup-coop-par"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([HARNESS, str(setup), "par", "coop", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 1 and "error: cmpc_create" in r.stderr, r.stderr
+
+
 def test_setup_writer_roundtrip(tmp_path):
     """The written file parses back (Python mirror of read_files.h) to the fixture."""
     from cmpc.configs import SetupFile
@@ -101,3 +117,42 @@ def test_gpu_cpp_adapter_step0_matches_reference(name, observer, tmp_path):
     u = [float(t) for t in r.stdout.split()]
     assert "status: " + " ".join(["0"] * cfg.S) in r.stderr, r.stderr
     GC.assert_six_digits(u, g["u0"])
+
+
+def read_dat(path):
+    lines = open(path).read().split("\n")
+    recs = []
+    for i in range(0, len(lines) - 5, 6):
+        recs.append({"t": lines[i], "x": lines[i + 1], "u": lines[i + 2], "y": lines[i + 3]})
+    return recs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser"])
+def test_gpu_cpp_harness_writes_reference_run(name, tmp_path):
+    """The whole 500 s run through the C++ adapter: all 10 000 records equal
+    the reference's (u, y to every printed digit, |v| < 1e-12 as 0; the
+    record times; the plant states of the first 160 records)."""
+    import json
+    import numpy as np
+    _build()
+    cfg, _, _, g = GC.case(name)
+    ctype, plant = name.split("-")
+    setup = tmp_path / f"setup-{name}"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([HARNESS, str(setup), plant, ctype, str(tmp_path)], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr
+    recs = read_dat(tmp_path / "parallel" / "out.dat")
+    key = {"cent": "centralized", "coop": "coop9", "ncoop": "ncoop9"}[ctype]
+    gold = np.load(os.path.join(HERE, "golden", "traj_long.npz"))
+    ur, yr = gold[f"{plant}_{key}_u"], gold[f"{plant}_{key}_y"]
+    assert len(recs) == len(ur) == 10000
+    six = lambda vals: ["0" if abs(float(v)) < 1e-12 else "%.6g" % float(v) for v in vals]
+    first = json.load(open(os.path.join(HERE, "golden", f"traj_{plant}_{key}.json")))["records"]
+    for k, rec in enumerate(recs):
+        assert float(rec["t"]) == float("%g" % (k * 0.05)), (k, rec["t"])
+        assert six(rec["u"].split()) == six(ur[k]), (k, rec["u"], ur[k])
+        assert six(rec["y"].split()) == six(yr[k]), (k, rec["y"], yr[k])
+        if k < len(first):
+            assert [float(v) for v in rec["x"].split()] == first[k]["x"], k
