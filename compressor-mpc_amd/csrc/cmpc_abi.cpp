@@ -66,6 +66,73 @@ int layout_of(const cmpc_dims* d, cmpc_layout* L) {
 
 thread_local LaunchEvents cmpc_launch_events;
 
+namespace {
+
+// Page-locked host buffer for the host-array entry points.  A hipMemcpy from or
+// to pageable memory costs ~17 us per call here: the runtime stages it through
+// its own bounce buffer (rocprofv3 --hip-trace of the B = 1 harness,
+// DESIGN.md §3.6).  From pinned memory it is one DMA.  `busy` is recorded after
+// the copies that read the buffer, and the next writer waits on it.
+struct PinnedIO {
+  char* buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t busy = nullptr;
+  bool pending = false;
+};
+
+int pinned_acquire(PinnedIO& p, size_t bytes) {
+  if (p.pending) {
+    HIP_TRY(hipEventSynchronize(p.busy));
+    p.pending = false;
+  }
+  if (bytes > p.cap) {
+    if (p.buf) HIP_TRY(hipHostFree(p.buf));
+    p.buf = nullptr;
+    p.cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 4096);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p.buf), cap, hipHostMallocDefault));
+    p.cap = cap;
+  }
+  return 0;
+}
+
+int pinned_release(PinnedIO& p, hipStream_t s) {
+  if (!p.busy) HIP_TRY(hipEventCreateWithFlags(&p.busy, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(p.busy, s));
+  p.pending = true;
+  return 0;
+}
+
+void pinned_free(PinnedIO& p) {
+  if (p.pending) (void)hipEventSynchronize(p.busy);
+  if (p.buf) (void)hipHostFree(p.buf);
+  if (p.busy) (void)hipEventDestroy(p.busy);
+  p = PinnedIO{};
+}
+
+// host -> device: the k arrays (nullptr skipped) are packed into `pin` and
+// copied by one DMA to `dev_base`; dev[i] receives each array's device address
+constexpr size_t kPad = 2;  // keep every array 16-byte aligned
+int pinned_upload(PinnedIO& pin, hipStream_t s, double* dev_base, const double* const* host,
+                  const size_t* n, int k, const double** dev) {
+  size_t tot = 0;
+  for (int i = 0; i < k; ++i) tot += host[i] ? (n[i] + kPad - 1) / kPad * kPad : 0;
+  if (pinned_acquire(pin, sizeof(double) * std::max<size_t>(tot, 1))) return -1;
+  double* h = reinterpret_cast<double*>(pin.buf);
+  size_t off = 0;
+  for (int i = 0; i < k; ++i) {
+    if (dev) dev[i] = nullptr;
+    if (!host[i]) continue;
+    std::memcpy(h + off, host[i], sizeof(double) * n[i]);
+    if (dev) dev[i] = dev_base + off;
+    off += (n[i] + kPad - 1) / kPad * kPad;
+  }
+  if (off) HIP_TRY(hipMemcpyAsync(dev_base, h, sizeof(double) * off, hipMemcpyHostToDevice, s));
+  return pinned_release(pin, s);
+}
+
+}  // namespace
+
 struct cmpc_ctx {
   cmpc_dims d{};
   cmpc_layout L{};
@@ -97,6 +164,7 @@ struct cmpc_ctx {
   double *d_obsM = nullptr, *obs = nullptr;
   double* stage = nullptr;  // host-pointer observer calls: device staging
   size_t stage_cap = 0;
+  PinnedIO pin_in, pin_out;  // host-array calls: page-locked staging
   int64_t obs_steps = 0;  // a-priori steps since cmpc_observer_init: the delay blocks' ring phase
   int obs_io[CMPC_MAX_S_PRODUCE][CMPC_MAX_INPUTS] = {};
   int obs_oi[CMPC_MAX_S_PRODUCE][4] = {};
@@ -338,6 +406,8 @@ int cmpc_destroy(cmpc_ctx* c) {
       (void)hipEventDestroy(pr.second);
     }
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+  pinned_free(c->pin_in);
+  pinned_free(c->pin_out);
   void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
                   c->ws,  c->status, c->nwsr, c->trace, c->ntrace, c->obs, c->d_obsM,
                   c->stage};
@@ -730,16 +800,9 @@ static int stage_host(cmpc_ctx* c, const double* const* host, const size_t* n, i
     HIP_TRY(hipMalloc(&c->stage, sizeof(double) * tot));
     c->stage_cap = tot;
   }
-  size_t off = 0;
-  for (int i = 0; i < k; ++i) {
-    dev[i] = nullptr;
-    if (!host[i]) continue;
-    HIP_TRY(hipMemcpyAsync(c->stage + off, host[i], sizeof(double) * n[i], hipMemcpyHostToDevice,
-                           c->stream));
-    dev[i] = c->stage + off;
-    off += (n[i] + 1) / 2 * 2;
-  }
-  return 0;
+  // one DMA from page-locked memory (the device stage is read by kernels
+  // queued after the copy on the same stream)
+  return pinned_upload(c->pin_in, c->stream, c->stage, host, n, k, dev);
 }
 
 int cmpc_observer_init_host(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
@@ -782,6 +845,7 @@ struct cmpc_sim {
   double *x = nullptr, *dt = nullptr, *u_full = nullptr, *u_offset = nullptr, *ring = nullptr,
          *scratch = nullptr, *stage = nullptr;  // stage: host-variant staging (B x max(ns, ni, no, nc))
   int32_t *cur = nullptr, *status = nullptr;
+  PinnedIO pin_in, pin_out;  // host-array calls: page-locked staging
 };
 
 int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, double p_out,
@@ -840,6 +904,8 @@ int cmpc_sim_destroy(cmpc_sim* m) {
   if (!m) return 0;
   (void)hipSetDevice(m->device);
   if (m->stream) (void)hipStreamSynchronize(m->stream);
+  pinned_free(m->pin_in);
+  pinned_free(m->pin_out);
   void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->cur, m->status};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -973,13 +1039,22 @@ int cmpc_sim_download(cmpc_sim* m, double* x, double* u_full, double* dt, int32_
   if (!m) return fail("null simulator");
   HIP_TRY(hipSetDevice(m->device));
   const size_t Bz = (size_t)m->B;
-  if (x) HIP_TRY(hipMemcpyAsync(x, m->x, sizeof(double) * Bz * m->ns, hipMemcpyDeviceToHost, m->stream));
-  if (u_full)
-    HIP_TRY(hipMemcpyAsync(u_full, m->u_full, sizeof(double) * Bz * m->ni, hipMemcpyDeviceToHost, m->stream));
-  if (dt) HIP_TRY(hipMemcpyAsync(dt, m->dt, sizeof(double) * Bz, hipMemcpyDeviceToHost, m->stream));
-  if (status)
-    HIP_TRY(hipMemcpyAsync(status, m->status, sizeof(int32_t) * Bz, hipMemcpyDeviceToHost, m->stream));
+  const size_t bx = sizeof(double) * Bz * m->ns, bu = sizeof(double) * Bz * m->ni, bd = sizeof(double) * Bz,
+               bs = sizeof(int32_t) * Bz;
+  auto up = [](size_t v) { return (v + 15) / 16 * 16; };
+  const size_t ou = up(bx), od = ou + up(bu), os = od + up(bd);
+  // device -> page-locked buffer (DMA), then host copies after one sync
+  if (pinned_acquire(m->pin_out, os + bs)) return -1;
+  char* h = m->pin_out.buf;
+  if (x) HIP_TRY(hipMemcpyAsync(h, m->x, bx, hipMemcpyDeviceToHost, m->stream));
+  if (u_full) HIP_TRY(hipMemcpyAsync(h + ou, m->u_full, bu, hipMemcpyDeviceToHost, m->stream));
+  if (dt) HIP_TRY(hipMemcpyAsync(h + od, m->dt, bd, hipMemcpyDeviceToHost, m->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(h + os, m->status, bs, hipMemcpyDeviceToHost, m->stream));
   HIP_TRY(hipStreamSynchronize(m->stream));
+  if (x) std::memcpy(x, h, bx);
+  if (u_full) std::memcpy(u_full, h + ou, bu);
+  if (dt) std::memcpy(dt, h + od, bd);
+  if (status) std::memcpy(status, h + os, bs);
   return 0;
 }
 
@@ -988,9 +1063,14 @@ int cmpc_sim_download(cmpc_sim* m, double* x, double* u_full, double* dt, int32_
 static int sim_stage(cmpc_sim* m, const double* h0, size_t n0, const double* h1, size_t n1) {
   HIP_TRY(hipSetDevice(m->device));
   const size_t half = (size_t)m->B * std::max(std::max(m->ns, m->ni), std::max(m->no, m->nc));
-  if (n0) HIP_TRY(hipMemcpyAsync(m->stage, h0, sizeof(double) * n0, hipMemcpyHostToDevice, m->stream));
-  if (n1) HIP_TRY(hipMemcpyAsync(m->stage + half, h1, sizeof(double) * n1, hipMemcpyHostToDevice, m->stream));
-  return 0;
+  // one DMA from page-locked memory: h0 at stage, h1 at stage + half
+  const size_t tot = n1 ? half + n1 : n0;
+  if (pinned_acquire(m->pin_in, sizeof(double) * std::max<size_t>(tot, 1))) return -1;
+  double* h = reinterpret_cast<double*>(m->pin_in.buf);
+  if (n0) std::memcpy(h, h0, sizeof(double) * n0);
+  if (n1) std::memcpy(h + half, h1, sizeof(double) * n1);
+  if (tot) HIP_TRY(hipMemcpyAsync(m->stage, h, sizeof(double) * tot, hipMemcpyHostToDevice, m->stream));
+  return pinned_release(m->pin_in, m->stream);
 }
 
 int cmpc_sim_reset_host(cmpc_sim* m, const double* x0, const double* u_offset, double dt0) {
@@ -1017,9 +1097,13 @@ int cmpc_sim_set_offset_host(cmpc_sim* m, const double* u_offset) {
 int cmpc_sim_output_host(cmpc_sim* m, double* y) {
   if (!m || !y) return fail("null argument");
   HIP_TRY(hipSetDevice(m->device));
+  const size_t by = sizeof(double) * (size_t)m->B * m->no;
+  if (pinned_acquire(m->pin_out, by)) return -1;
   if (cmpc_sim_output(m, m->stage)) return -1;
-  HIP_TRY(hipMemcpyAsync(y, m->stage, sizeof(double) * (size_t)m->B * m->no, hipMemcpyDeviceToHost, m->stream));
-  return cmpc_sim_synchronize(m);
+  HIP_TRY(hipMemcpyAsync(m->pin_out.buf, m->stage, by, hipMemcpyDeviceToHost, m->stream));
+  if (cmpc_sim_synchronize(m)) return -1;
+  std::memcpy(y, m->pin_out.buf, by);
+  return 0;
 }
 
 double* cmpc_sim_state(cmpc_sim* m) { return m ? m->x : nullptr; }
@@ -1375,10 +1459,18 @@ int cmpc_download(cmpc_ctx* c, double* du, int32_t* status, int32_t* nwsr) {
   if (!c) return fail("null context");
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)c->nqp;
-  if (du) HIP_TRY(hipMemcpyAsync(du, c->du, sizeof(double) * n * c->L.nV, hipMemcpyDeviceToHost, c->stream));
-  if (status) HIP_TRY(hipMemcpyAsync(status, c->status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-  if (nwsr) HIP_TRY(hipMemcpyAsync(nwsr, c->nwsr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  const size_t b_du = sizeof(double) * n * c->L.nV, b_i = sizeof(int32_t) * n;
+  const size_t o_st = (b_du + 15) / 16 * 16, o_nw = o_st + (b_i + 15) / 16 * 16;
+  // device -> page-locked buffer (DMA), then host copies after one sync
+  if (pinned_acquire(c->pin_out, o_nw + b_i)) return -1;
+  char* h = c->pin_out.buf;
+  if (du) HIP_TRY(hipMemcpyAsync(h, c->du, b_du, hipMemcpyDeviceToHost, c->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(h + o_st, c->status, b_i, hipMemcpyDeviceToHost, c->stream));
+  if (nwsr) HIP_TRY(hipMemcpyAsync(h + o_nw, c->nwsr, b_i, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (du) std::memcpy(du, h, b_du);
+  if (status) std::memcpy(status, h + o_st, b_i);
+  if (nwsr) std::memcpy(nwsr, h + o_nw, b_i);
   return 0;
 }
 
