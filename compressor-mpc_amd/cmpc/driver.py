@@ -113,8 +113,8 @@ class ClosedLoop:
         torch = self.torch
         u_default = np.asarray(u_default, dtype=np.float64)
         # per-scenario defaults and changes broadcast: (n_inputs,) or (B, n_inputs)
-        offs = [np.array(np.broadcast_to(u_default + np.asarray(d, dtype=np.float64), (self.B, u_default.shape[-1])))
-                for d, _ in segments]
+        shape = (self.B, u_default.shape[-1])
+        offs = [np.array(np.broadcast_to(u_default + np.asarray(d, dtype=np.float64), shape)) for d, _ in segments]
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
         self.u_offset = t(offs[0])
         self._sched = [(float(segments[i - 1][1]), t(offs[i])) for i in range(1, len(segments))]
@@ -138,7 +138,6 @@ class ClosedLoop:
         """One sampling instant: returns (t, y) of the instant; the plant has
         advanced to the next one."""
         from ._abi import check, iptr
-        torch = self.torch
         t = 0.0 + self.k * self.Ts   # the record's label (record count)
         # integrate_const's own time: start_time + step * dt of the current
         # Integrate call; its interval ends at time + dt
