@@ -152,6 +152,8 @@ struct cmpc_ctx {
          *du = nullptr;
   uint32_t* ws = nullptr;
   int32_t *status = nullptr, *nwsr = nullptr, *ntrace = nullptr;
+  char* out_block = nullptr;  // du | status | nwsr in one allocation: one D2H for cmpc_download
+  size_t out_st = 0, out_nw = 0, out_len = 0;  // byte offsets of status, nwsr; block length
   uint8_t* trace = nullptr;
   size_t trace_cap = 0;
   int trace_K = 0;
@@ -377,11 +379,19 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
       hipMalloc(&c->cfg, sizeof(double) * (size_t)S * c->co.len) != hipSuccess ||
       hipMalloc(&c->u_old, sizeof(double) * n * d.nu_tot) != hipSuccess ||
       hipMalloc(&c->du_old, sizeof(double) * n * L.nV) != hipSuccess ||
-      hipMalloc(&c->du, sizeof(double) * n * L.nV) != hipSuccess ||
-      hipMalloc(&c->ws, sizeof(uint32_t) * n) != hipSuccess ||
-      hipMalloc(&c->status, sizeof(int32_t) * n) != hipSuccess ||
-      hipMalloc(&c->nwsr, sizeof(int32_t) * n) != hipSuccess)
+      hipMalloc(&c->ws, sizeof(uint32_t) * n) != hipSuccess)
     return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
+  {
+    auto up16 = [](size_t v) { return (v + 15) / 16 * 16; };
+    c->out_st = up16(sizeof(double) * n * L.nV);
+    c->out_nw = c->out_st + up16(sizeof(int32_t) * n);
+    c->out_len = c->out_nw + sizeof(int32_t) * n;
+    if (hipMalloc(&c->out_block, c->out_len) != hipSuccess)
+      return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
+    c->du = reinterpret_cast<double*>(c->out_block);
+    c->status = reinterpret_cast<int32_t*>(c->out_block + c->out_st);
+    c->nwsr = reinterpret_cast<int32_t*>(c->out_block + c->out_nw);
+  }
   if (hipMemsetAsync(c->lin, 0, sizeof(double) * n * L.rec_len, c->stream) != hipSuccess ||
       hipMemsetAsync(c->qp, 0, sizeof(double) * n * c->qp_len, c->stream) != hipSuccess ||
       hipMemsetAsync(c->u_old, 0, sizeof(double) * n * d.nu_tot, c->stream) != hipSuccess ||
@@ -408,8 +418,8 @@ int cmpc_destroy(cmpc_ctx* c) {
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   pinned_free(c->pin_in);
   pinned_free(c->pin_out);
-  void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->du,
-                  c->ws,  c->status, c->nwsr, c->trace, c->ntrace, c->obs, c->d_obsM,
+  void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->out_block,
+                  c->ws,  c->trace, c->ntrace, c->obs, c->d_obsM,
                   c->stage};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1460,13 +1470,18 @@ int cmpc_download(cmpc_ctx* c, double* du, int32_t* status, int32_t* nwsr) {
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)c->nqp;
   const size_t b_du = sizeof(double) * n * c->L.nV, b_i = sizeof(int32_t) * n;
-  const size_t o_st = (b_du + 15) / 16 * 16, o_nw = o_st + (b_i + 15) / 16 * 16;
-  // device -> page-locked buffer (DMA), then host copies after one sync
-  if (pinned_acquire(c->pin_out, o_nw + b_i)) return -1;
+  const size_t o_st = c->out_st, o_nw = c->out_nw;
+  // device -> page-locked buffer (DMA; one copy of the du | status | nwsr
+  // block when all are asked for), then host copies after one sync
+  if (pinned_acquire(c->pin_out, c->out_len)) return -1;
   char* h = c->pin_out.buf;
-  if (du) HIP_TRY(hipMemcpyAsync(h, c->du, b_du, hipMemcpyDeviceToHost, c->stream));
-  if (status) HIP_TRY(hipMemcpyAsync(h + o_st, c->status, b_i, hipMemcpyDeviceToHost, c->stream));
-  if (nwsr) HIP_TRY(hipMemcpyAsync(h + o_nw, c->nwsr, b_i, hipMemcpyDeviceToHost, c->stream));
+  if (du && status && nwsr) {
+    HIP_TRY(hipMemcpyAsync(h, c->out_block, c->out_len, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    if (du) HIP_TRY(hipMemcpyAsync(h, c->du, b_du, hipMemcpyDeviceToHost, c->stream));
+    if (status) HIP_TRY(hipMemcpyAsync(h + o_st, c->status, b_i, hipMemcpyDeviceToHost, c->stream));
+    if (nwsr) HIP_TRY(hipMemcpyAsync(h + o_nw, c->nwsr, b_i, hipMemcpyDeviceToHost, c->stream));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (du) std::memcpy(du, h, b_du);
   if (status) std::memcpy(status, h + o_st, b_i);
