@@ -176,6 +176,10 @@ def load_library(path: str = LIB_PATH):
         "cmpc_sim_output": ([c_void, c_void], ctypes.c_int),
         "cmpc_sim_synchronize": ([c_void], ctypes.c_int),
         "cmpc_sim_download": ([c_void, P(dbl), P(dbl), P(dbl), P(i32)], ctypes.c_int),
+        "cmpc_sim_reset_host": ([c_void, P(dbl), P(dbl), dbl], ctypes.c_int),
+        "cmpc_sim_set_input_host": ([c_void, P(dbl)], ctypes.c_int),
+        "cmpc_sim_set_offset_host": ([c_void, P(dbl)], ctypes.c_int),
+        "cmpc_sim_output_host": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_sim_state": ([c_void], c_void),
         "cmpc_sim_input": ([c_void], c_void),
         "cmpc_sim_step_size": ([c_void], c_void),
