@@ -111,6 +111,11 @@ def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
                    f"(reference op order, -O3, OpenMP), {dt * reps:.1f} s"),
         "single_thread_value": probe * S * K / t_single,
         "single_thread_us_per_scenario_step": t_single / probe * 1e6,
+        "reference_recorded": {
+            "note": "context, not comparison (BASELINE.md §1): the reference's own per-step wall "
+                    "times from results/parallel/run*/coop{1,9}.dat, p = 100, one thread, CPU unrecorded",
+            "coop9_step_us": 900.4, "coop1_step_us": 727.2, "build_us_per_subcontroller": 349.0,
+            "resolve_us_per_qp": 10.7, "qp_solves_per_s_k9": 20.0e3},
     }
 
 
