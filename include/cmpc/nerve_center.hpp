@@ -24,9 +24,11 @@
 //    reference.  Each sub-controller's observer (observer.cc:6-40), its
 //    linearisation at its own estimate, the QP build, K Jacobi iterations and
 //    UpdateU run on the GPU, the state estimates resident in device memory.
+//    The reference runs' M is ReferenceObserverGain(spec) = [0; I] (set in
+//    the harness's missing common-simulation.inc, identified from the
+//    recorded runs).
 //  - with an external estimate: GetNextInput(y, x_hat, dx_aug) takes the state
-//    estimate from the caller (the reference harness's gain M lives in its
-//    missing common-simulation.inc); the linearisation runs on the host
+//    estimate from the caller; the linearisation runs on the host
 //    (cmpc_plant_lin_record), the rest on the GPU.
 #pragma once
 
