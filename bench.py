@@ -398,12 +398,24 @@ def main():
                     loop.step()
                 torch.cuda.synchronize(local)
                 t_p = (time.perf_counter() - t0) / reps_p
+                # the same steps again with the library's kernels event-timed
+                loop.ctx.enable_timing(True)
+                for _ in range(reps_p):
+                    loop.step()
+                torch.cuda.synchronize(local)
+                lk = lambda k: loop.ctx.kernel_time(k)[0] / max(loop.ctx.kernel_time(k)[1], 1)
+                plant_kernels = {"observe_post": lk(cmpc.CMPC_KERNEL_OBSERVE_POST),
+                                 "produce_per_qp": lk(cmpc.CMPC_KERNEL_PRODUCE),
+                                 "build": lk(cmpc.CMPC_KERNEL_BUILD), "iterate": lk(cmpc.CMPC_KERNEL_ITERATE),
+                                 "observe_prior": lk(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
+                loop.ctx.enable_timing(False)
                 _, st_p, _ = loop.ctx.download()
                 _, _, _, sst = loop.sim.download()
             finally:
                 loop.close()
             closed["with_plant"] = {
                 "ms_per_step": t_p * 1e3, "scenario_steps_per_s": B / t_p, "qp_solves_per_s": B * S * K / t_p,
+                "kernels_ms": plant_kernels,
                 "qp_status_ok_fraction": float((st_p == 0).mean()), "plant_step_failures": int((sst != 0).sum()),
                 "steps": reps_p,
                 "note": "cmpc.driver.ClosedLoop: y = plant output, observe a posteriori + per-QP "
