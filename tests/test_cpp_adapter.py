@@ -30,8 +30,9 @@ def _mat(vals, n):
     return "\n".join("\t".join("%g" % v for v in vals[r * n:(r + 1) * n]) for r in range(n))
 
 
-def write_setup(path, g, ny, S):
-    """setup/setup-<ctrl>-<plant> layout (key line, values, blank line)."""
+def write_setup(path, g, ny, S, n_timing=None):
+    """setup/setup-<ctrl>-<plant> layout (key line, values, blank line);
+    n_timing: n-timing-iterations (run-all-tests.sh sweeps it 1..9)."""
     nci = int(round(len(g["uwt"]) ** 0.5))
     blk = ny * ny
     yw = g["ywt"]
@@ -41,7 +42,7 @@ def write_setup(path, g, ny, S):
     segs = [(sim[i:i + n - 1], sim[i + n - 1]) for i in range(0, len(sim), n)]
     parts = [
         ("n-iterations", str(g["n_iterations"])),
-        ("n-timing-iterations", str(g["n_iterations"])),
+        ("n-timing-iterations", str(g["n_iterations"] if n_timing is None else n_timing)),
         ("folder-name", "parallel"),
         ("output-filename", "out.dat"),
         ("yref", " ".join("%g" % v for v in g["yref"])),
@@ -156,3 +157,27 @@ def test_gpu_cpp_harness_writes_reference_run(name, tmp_path):
         assert six(rec["y"].split()) == six(yr[k]), (k, rec["y"], yr[k])
         if k < len(first):
             assert [float(v) for v in rec["x"].split()] == first[k]["x"], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_timing", [1, 4])
+def test_gpu_cpp_harness_timed_prefix_keeps_trajectory(n_timing, tmp_path):
+    """setup/run-all-tests.sh runs coop with n-timing-iterations 1..9 and the
+    reference's coop1..coop9 files hold one trajectory: the
+    timed prefix splits the K Jacobi iterations into two launches without
+    changing a record (first 1 200 records, across the 50 s step)."""
+    import numpy as np
+    _build()
+    cfg, _, _, g = GC.case("coop-par")
+    setup = tmp_path / "setup-coop-par"
+    write_setup(setup, g, cfg.ny, cfg.S, n_timing=n_timing)
+    r = subprocess.run([HARNESS, str(setup), "par", "coop", str(tmp_path), "1200"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    recs = read_dat(tmp_path / "parallel" / "out.dat")
+    gold = np.load(os.path.join(HERE, "golden", "traj_long.npz"))
+    ur = gold["par_coop9_u"]
+    six = lambda vals: ["0" if abs(float(v)) < 1e-12 else "%.6g" % float(v) for v in vals]
+    assert len(recs) == 1200
+    for k, rec in enumerate(recs):
+        assert six(rec["u"].split()) == six(ur[k]), (k, rec["u"], ur[k])
