@@ -94,7 +94,8 @@ EXPORTS = (
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
     "cmpc_observer_init_host", "cmpc_observe_step_host",
     "cmpc_sim_create", "cmpc_sim_destroy", "cmpc_sim_set_stream", "cmpc_sim_reset",
-    "cmpc_sim_set_input", "cmpc_sim_set_offset", "cmpc_sim_restart", "cmpc_sim_plant_input", "cmpc_sim_integrate", "cmpc_sim_output",
+    "cmpc_sim_set_input", "cmpc_sim_set_offset", "cmpc_sim_restart", "cmpc_sim_plant_input_offset",
+    "cmpc_sim_plant_input", "cmpc_sim_integrate", "cmpc_sim_output",
     "cmpc_sim_synchronize", "cmpc_sim_state", "cmpc_sim_input", "cmpc_sim_step_size",
     "cmpc_sim_status", "cmpc_accumulate_moves", "cmpc_sim_download", "cmpc_sim_reset_host",
     "cmpc_sim_set_input_host", "cmpc_sim_set_offset_host", "cmpc_sim_output_host",
@@ -171,6 +172,7 @@ def load_library(path: str = LIB_PATH):
         "cmpc_sim_set_input": ([c_void, c_void], ctypes.c_int),
         "cmpc_sim_set_offset": ([c_void, c_void], ctypes.c_int),
         "cmpc_sim_restart": ([c_void, ctypes.c_double], ctypes.c_int),
+        "cmpc_sim_plant_input_offset": ([c_void, c_void, c_void, c_void], ctypes.c_int),
         "cmpc_sim_plant_input": ([c_void, c_void, c_void], ctypes.c_int),
         "cmpc_sim_integrate": ([c_void, dbl, dbl, dbl, dbl], ctypes.c_int),
         "cmpc_sim_output": ([c_void, c_void], ctypes.c_int),

@@ -98,7 +98,6 @@ class ClosedLoop:
         self.x0, self.u_offset = t(x0), t(u_offset)
         self.u_ctrl = torch.zeros(B, cfg.nu_tot, dtype=torch.float64, device=dev)  # NerveCenter::u_old_
         self.u_lin = torch.zeros_like(self.u_offset)   # GetPlantInput(u_old_, u_offset_)
-        self.cidx = torch.tensor(REF_CONTROL_INDEX, dtype=torch.long, device=dev)
         self.io = np.ascontiguousarray(cfg.input_order, dtype=np.int32)
         self.k = 0
         self._sched = []   # pending (t_start, plant-input offset (B, n_inputs) device)
@@ -146,8 +145,7 @@ class ClosedLoop:
         # GetNextInputWithTiming(y): linearisation input GetPlantInput(u_old_,
         # u_offset_) with the controller's own offset (fixed at Initialize; the
         # plant's may have stepped, see set_segments)
-        self.u_lin.copy_(self.u_offset)
-        self.u_lin[:, self.cidx] += self.u_ctrl
+        self.sim.plant_input_offset(self.u_ctrl, self.u_offset, self.u_lin)
         self.ctx.observe_step(self.u_lin.data_ptr(), y.data_ptr())
         self.ctx.build()
         self.ctx.iterate(self.K)

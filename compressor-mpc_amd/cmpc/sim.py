@@ -83,6 +83,13 @@ class PlantSimulator:
         """A new Integrate call: the carried step size starts again at dt0."""
         check(self.lib.cmpc_sim_restart(self._h, dt0), "cmpc_sim_restart")
 
+    def plant_input_offset(self, u_control, u_offset, out):
+        """GetPlantInput over a given offset (the controller's u_offset_)."""
+        check(self.lib.cmpc_sim_plant_input_offset(self._h, ctypes.c_void_p(u_control.data_ptr()),
+                                                   ctypes.c_void_p(u_offset.data_ptr()),
+                                                   ctypes.c_void_p(out.data_ptr())),
+              "cmpc_sim_plant_input_offset")
+
     def plant_input(self, u_control, out):
         """GetPlantInput without the delay line into out (B, n_inputs)."""
         check(self.lib.cmpc_sim_plant_input(self._h, ctypes.c_void_p(u_control.data_ptr()),

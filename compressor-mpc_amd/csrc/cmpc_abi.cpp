@@ -848,13 +848,14 @@ int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
 // ---- plant simulation ----
 struct cmpc_sim {
   int plant = 0, B = 0, device = 0, ns = 0, ni = 0, no = 0, nc = 0, ring_len = 0;
+  int cur[CMPC_MAX_INPUTS] = {};  // TimeDelay cursors (every scenario's are the same)
   double p_in = 1.0, p_out = 1.0;
   int delay[CMPC_MAX_INPUTS] = {}, cidx[CMPC_MAX_INPUTS] = {};
   hipStream_t stream = nullptr;
   bool own_stream = false;
   double *x = nullptr, *dt = nullptr, *u_full = nullptr, *u_offset = nullptr, *ring = nullptr,
          *scratch = nullptr, *stage = nullptr;  // stage: host-variant staging (B x max(ns, ni, no, nc))
-  int32_t *cur = nullptr, *status = nullptr;
+  int32_t* status = nullptr;
   PinnedIO pin_in, pin_out;  // host-array calls: page-locked staging
 };
 
@@ -884,7 +885,7 @@ int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, d
   if (m->ring_len == 0) m->ring_len = 1;
   auto bail = [&](hipError_t e) {
     (void)e;
-    void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->cur, m->status};
+    void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->status};
     for (void* b : bufs)
       if (b) (void)hipFree(b);
     delete m;
@@ -903,7 +904,6 @@ int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, d
       (e = hipMalloc(&m->scratch, sizeof(double) * Bz * (ni > n_control ? ni : n_control))) != hipSuccess ||
       (e = hipMalloc(&m->stage, sizeof(double) * Bz * 2 * std::max(std::max(ns, ni), std::max(no, n_control)))) !=
           hipSuccess ||
-      (e = hipMalloc(&m->cur, sizeof(int32_t) * Bz * n_control)) != hipSuccess ||
       (e = hipMalloc(&m->status, sizeof(int32_t) * Bz)) != hipSuccess)
     return bail(e);
   *out = m;
@@ -916,7 +916,7 @@ int cmpc_sim_destroy(cmpc_sim* m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   pinned_free(m->pin_in);
   pinned_free(m->pin_out);
-  void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->cur, m->status};
+  void* bufs[] = {m->x, m->dt, m->u_full, m->u_offset, m->ring, m->scratch, m->stage, m->status};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (m->own_stream && m->stream) (void)hipStreamDestroy(m->stream);
@@ -941,7 +941,6 @@ static SimInputParams sim_input_params(cmpc_sim* m, const double* u_control, int
   P.u_offset = m->u_offset;
   P.u_full = m->u_full;
   P.ring = m->ring;
-  P.cur = m->cur;
   P.B = m->B;
   P.nc = m->nc;
   P.ni = m->ni;
@@ -950,6 +949,7 @@ static SimInputParams sim_input_params(cmpc_sim* m, const double* u_control, int
   for (int i = 0; i < m->nc; ++i) {
     P.delay[i] = m->delay[i];
     P.cidx[i] = m->cidx[i];
+    P.cur[i] = m->cur[i];
   }
   return P;
 }
@@ -966,15 +966,10 @@ int cmpc_sim_reset(cmpc_sim* m, const double* x0, const double* u_offset, double
   HIP_TRY(hipMemcpyAsync(m->dt, dts.data(), sizeof(double) * Bz, hipMemcpyHostToDevice, m->stream));
   // TimeDelay(): zero memory, cursor of input i at the sum of the delays before it
   HIP_TRY(hipMemsetAsync(m->ring, 0, sizeof(double) * Bz * m->ring_len, m->stream));
-  std::vector<int32_t> cur(Bz * m->nc);
-  for (size_t b = 0; b < Bz; ++b) {
-    int sum = 0;
-    for (int i = 0; i < m->nc; ++i) {
-      cur[b * m->nc + i] = sum;
-      sum += m->delay[i];
-    }
+  for (int i = 0, sum = 0; i < m->nc; ++i) {
+    m->cur[i] = sum;
+    sum += m->delay[i];
   }
-  HIP_TRY(hipMemcpyAsync(m->cur, cur.data(), sizeof(int32_t) * cur.size(), hipMemcpyHostToDevice, m->stream));
   // u_ = GetPlantInput(u_init = 0) = u_offset
   HIP_TRY(hipMemcpyAsync(m->u_full, u_offset, sizeof(double) * Bz * m->ni, hipMemcpyDeviceToDevice,
                          m->stream));
@@ -987,7 +982,14 @@ int cmpc_sim_set_input(cmpc_sim* m, const double* u_control) {
   HIP_TRY(hipSetDevice(m->device));
   const SimInputParams P = sim_input_params(m, u_control, 1);
   if (cmpc_launch_sim_input(P, m->stream)) return fail("sim input launch failed");
-  return check_launch("sim input kernel");
+  if (check_launch("sim input kernel")) return -1;
+  // TimeDelay::GetDelayedInput's cursor step (time_delay.h:41-58), on the host
+  for (int i = 0, end = 0; i < m->nc; ++i) {
+    if (m->delay[i] == 0) continue;
+    end += m->delay[i];
+    if (++m->cur[i] == end) m->cur[i] -= m->delay[i];
+  }
+  return 0;
 }
 
 int cmpc_sim_set_offset(cmpc_sim* m, const double* u_offset) {
@@ -996,6 +998,17 @@ int cmpc_sim_set_offset(cmpc_sim* m, const double* u_offset) {
   HIP_TRY(hipMemcpyAsync(m->u_offset, u_offset, sizeof(double) * (size_t)m->B * m->ni,
                          hipMemcpyDeviceToDevice, m->stream));
   return 0;
+}
+
+int cmpc_sim_plant_input_offset(cmpc_sim* m, const double* u_control, const double* u_offset,
+                                double* u_full_out) {
+  if (!m || !u_control || !u_offset || !u_full_out) return fail("null argument");
+  HIP_TRY(hipSetDevice(m->device));
+  SimInputParams P = sim_input_params(m, u_control, 0);
+  P.u_offset = u_offset;
+  P.u_full = u_full_out;
+  if (cmpc_launch_sim_input(P, m->stream)) return fail("sim input launch failed");
+  return check_launch("sim input kernel");
 }
 
 int cmpc_sim_restart(cmpc_sim* m, double dt0) {

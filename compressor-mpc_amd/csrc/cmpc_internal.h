@@ -209,11 +209,11 @@ struct SimInputParams {
   const double* u_control;  // B * nc
   const double* u_offset;   // B * ni
   double* u_full;           // B * ni
-  double* ring;             // B * ring_len
-  int32_t* cur;             // B * nc
+  double* ring;             // ring_len * B, slot-major: slot k of every scenario is contiguous
   int B, nc, ni, ring_len, use_delay;
   int delay[CMPC_MAX_INPUTS];
   int cidx[CMPC_MAX_INPUTS];
+  int cur[CMPC_MAX_INPUTS];  // ring slot of each delayed input (the same for every scenario)
 };
 struct AccumParams {
   const double* du;   // nqp * nV

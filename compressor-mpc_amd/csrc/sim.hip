@@ -139,25 +139,21 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
 }
 
 // SetInput: TimeDelay::GetDelayedInput then GetPlantInput (u_offset + delayed
-// control input at ControlInputIndex); ring/cursor per scenario
+// control input at ControlInputIndex).  Every scenario's delay line advances
+// in step, so the cursors are the host's (P.cur) and the ring is slot-major:
+// the read and the write of a slot coalesce across the scenarios of a wave.
 __global__ __launch_bounds__(64) void cmpc_sim_input_kernel(SimInputParams P) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= P.B) return;
-  double* ring = P.ring + (size_t)b * P.ring_len;
-  int32_t* cur = P.cur + (size_t)b * P.nc;
   double out[CMPC_MAX_INPUTS];
-  int index_delay_states = 0;
   for (int i = 0; i < P.nc; ++i) {
     const double un = P.u_control[(size_t)b * P.nc + i];
     if (P.delay[i] == 0 || !P.use_delay) {
       out[i] = un;
     } else {
-      index_delay_states += P.delay[i];
-      int c = cur[i];
-      out[i] = ring[c];
-      ring[c] = un;
-      if (++c == index_delay_states) c -= P.delay[i];
-      cur[i] = c;
+      double* slot = P.ring + (size_t)P.cur[i] * P.B + b;
+      out[i] = *slot;
+      *slot = un;
     }
   }
   double* uf = P.u_full + (size_t)b * P.ni;

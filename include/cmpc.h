@@ -312,6 +312,9 @@ int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
  *   cmpc_sim_output     GetOutput() (B x n_outputs, device)
  *   cmpc_sim_plant_input GetPlantInput(u_control) without the delay line (the
  *                       controller's linearisation input, nerve_center.h:139)
+ *   cmpc_sim_plant_input_offset  the same over a given offset (B x n_inputs,
+ *                       device): the controller's own u_offset_, which keeps
+ *                       its Initialize value when the plant's steps
  * Device arrays: cmpc_sim_state (x), cmpc_sim_input (plant input u_),
  * cmpc_sim_step_size (dt), cmpc_sim_status (1 = step-size control failed:
  * 500 rejected tries of one step; 2 = more than 500 steps in one interval,
@@ -327,6 +330,8 @@ int cmpc_sim_set_input(cmpc_sim* sim, const double* u_control);
 int cmpc_sim_set_offset(cmpc_sim* sim, const double* u_offset);
 int cmpc_sim_restart(cmpc_sim* sim, double dt0);
 int cmpc_sim_plant_input(cmpc_sim* sim, const double* u_control, double* u_full_out);
+int cmpc_sim_plant_input_offset(cmpc_sim* sim, const double* u_control, const double* u_offset,
+                                double* u_full_out);
 int cmpc_sim_integrate(cmpc_sim* sim, double t, double t_end, double eps_abs, double eps_rel);
 int cmpc_sim_output(cmpc_sim* sim, double* y);
 int cmpc_sim_synchronize(cmpc_sim* sim);
