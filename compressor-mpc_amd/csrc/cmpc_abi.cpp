@@ -677,7 +677,9 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
   HIP_TRY(hipSetDevice(c->device));
   if (!c->obs) {
     c->obs_nout = n_outputs;
-    c->obs_len = (d.ns + c->L.ntot + n_outputs + n_outputs * d.ns + 1) / 2 * 2;
+    // rows padded to 128 B (16 doubles): every row starts on a cache line, so
+    // the observer kernels' field reads touch no line shared with a neighbour
+    c->obs_len = (d.ns + c->L.ntot + n_outputs + n_outputs * d.ns + 15) / 16 * 16;
     c->obsM.assign((size_t)d.S * c->L.nobs * n_outputs, 0.0);
     c->have_M.assign(d.S, 0);
     HIP_TRY(hipMalloc(&c->d_obsM, sizeof(double) * c->obsM.size()));

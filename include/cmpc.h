@@ -242,8 +242,9 @@ int cmpc_coupled_iterate(cmpc_ctx* ctx, int S_total, int S_local, int s_offset,
  * row 2).  Each QP slot keeps the state of its sub-controller's
  * DistributedController (observer.h:53-56, distributed_controller.h:104-111)
  * in HBM, a row of cmpc_observer_len() doubles:
- *   [x_hat ns][dx_aug ntot][y_old n_outputs][C n_outputs x ns]
- * (ntot = ns + ndist + delay states, the full AugmentedState; C = the plant
+ *   [x_hat ns][dx_aug ntot][y_old n_outputs][C n_outputs x ns][padding]
+ * (rows padded to a multiple of 16 doubles, one 128-byte line;
+ * ntot = ns + ndist + delay states, the full AugmentedState; C = the plant
  * output matrix of the last linearisation).  A closed-loop control step is
  *   cmpc_observe_step(u_full, y)   ObserveAPosteriori + x_ += (observer.cc:27-44,
  *                                  distributed_controller.cc:80), then

@@ -160,9 +160,10 @@ def _torch_first(request):
     yield
 
 
-def split(cfg, L, st):
+def split(cfg, L, st, n_out=4):
+    """An observer row [x_hat ns][dx_aug ntot][y_old n_out][C n_out x ns]
+    (+ padding to the row stride)."""
     ns, ntot = cfg.ns, L.ntot
-    n_out = (st.shape[1] - ns - ntot) // (1 + ns)
     xh = st[:, :ns]
     dx = st[:, ns:ns + ntot]
     yo = st[:, ns + ntot:ns + ntot + n_out]
