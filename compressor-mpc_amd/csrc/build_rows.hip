@@ -548,6 +548,9 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
       per_cu < 1)
     per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   per_cu = std::min(per_cu, std::max(1, 4 * CMPC_ROWS_WPE / WPG));  // ablation: fewer waves per SIMD
+  // the occupancy query counts the requested LDS only; the measured
+  // allocation model (rows_layout.cpp) can allow fewer
+  per_cu = std::max(1, std::min(per_cu, cmpc_rows_resident_groups(P.rows, WPG)));
   const int need = std::max(1, ((P.nqp + 3) / 4 + WPG - 1) / WPG);
   const int grid = std::max(1, std::min(need, P.cus * per_cu));
   cmpc_launch(kern, dim3(grid), dim3(64 * WPG), lds, s, P);

@@ -188,6 +188,8 @@ int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
 // Waves per workgroup the row kernel launches with for layout R (4, 2 or 1;
 // 0: does not fit) (build_rows.hip).
 int cmpc_rows_waves_per_group(const RowsLayout& R);
+// workgroups of w waves per CU that the layout's LDS lets run at once
+int cmpc_rows_resident_groups(const RowsLayout& R, int w);
 // LDS layout of the row kernel, chosen by a bank-conflict model of its
 // horizon loop (rows_layout.cpp); cached per dimension set, thread-safe.
 void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLayout* out);

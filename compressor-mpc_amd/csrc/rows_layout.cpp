@@ -234,9 +234,13 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
 // resident waves per CU of layout R with w waves per workgroup, at most 12
 // (3 waves/SIMD: the kernel's register budget)
 int waves_with(const RowsLayout& R, int w) {
-  // LDS is allocated in granules: count whole KiB (a layout 80 bytes over a
-  // third of the LDS measured as 2 resident workgroups, ser-cent p = 50)
-  const size_t lds = (sizeof(double) * ((size_t)R.lds_block + (size_t)R.per_wave * w) + 1023) / 1024 * 1024;
+  // A workgroup takes more LDS than it asks for.  Measured residency: 54 240 B
+  // per workgroup runs as 2 per CU (ser-coop p = 50: 3 requested by the
+  // occupancy query, 0.382 ms; 2 forced, 0.350 ms), 53 408 B as 3 (ser-cent
+  // p = 50), 81 168 B as 2 (par-coop p = 100), 54 693 B as 2.  Model: the
+  // request rounded up to 512 B, plus 512 B.
+  const size_t req = sizeof(double) * ((size_t)R.lds_block + (size_t)R.per_wave * w);
+  const size_t lds = (req + 511) / 512 * 512 + 512;
   return lds <= (size_t)kLdsBytes ? std::min(12, (int)(kLdsBytes / lds) * w) : 0;
 }
 
@@ -263,6 +267,8 @@ uint64_t lcg(uint64_t& s) {
 // ser-cent 4 vs 6 waves 0.49 vs 0.80 ms; tools/gpu_wpg_sweep.sh).  0 when
 // not even one two-wave workgroup per SIMD fits: the one-QP-per-wave kernel
 // runs.  CMPC_ROWS_WPG=4|2 overrides it for timing.
+int cmpc_rows_resident_groups(const RowsLayout& R, int w) { return w > 0 ? waves_with(R, w) / w : 0; }
+
 int cmpc_rows_waves_per_group(const RowsLayout& R) {
   if (const char* e = std::getenv("CMPC_ROWS_WPG")) {
     const int w = std::atoi(e);
