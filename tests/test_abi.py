@@ -112,9 +112,14 @@ def test_rows_lds_layout_search(plant, ctype, p):
     packed, chosen, nbytes = cmpc.rows_lds_model(CmpcDims.from_config(cfg, 8))
     assert chosen <= packed
     assert 0 < nbytes <= 160 * 1024
+    # LDS a workgroup occupies (measured model, rows_layout.cpp): the request
+    # rounded up to 512 B, plus 512 B
+    alloc = (nbytes + 511) // 512 * 512 + 512
     if (plant, ctype, p) == ("par", "coop", 50):
         assert packed > 20 and chosen <= 3.0
-        assert 160 * 1024 // nbytes >= 3  # the kernel runs three 4-wave workgroups per CU
+        assert 160 * 1024 // alloc >= 3  # the kernel runs three 4-wave workgroups per CU
+    if (plant, ctype, p) == ("ser", "coop", 50):
+        assert 160 * 1024 // alloc >= 3  # 54 240 B (two resident) before the model
 
 
 def test_rows_lds_model_python_mirror_agrees():
