@@ -139,7 +139,7 @@ def test_gpu_closed_loop_reproduces_reference_run(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["coop-par", "cent-ser", "ncoop-ser"])
+@pytest.mark.parametrize("name", list(TRAJ))
 def test_gpu_closed_loop_scenarios_match_oracle(name):
     """B = 6 different scenarios in one batch (perturbed initial states,
     each its own size of the plant-input step at 10 s), 600 instants, against
