@@ -5,8 +5,9 @@ path at horizon p = 50 (BASELINE.json metric) on MI355X.
 One step = one batched NerveCenter control step over B scenarios per GPU
 (2-compressor cooperative-parallel plant, S = 2 sub-controllers each, m = 2):
 condensed-QP build of every sub-controller (cmpc_build) + K = 9 Jacobi
-iterations of warm-started QP re-solves with the plan exchange
-(cmpc_iterate).  QP solves per step = B * S * K per GPU.
+iterations of warm-started QP re-solves with the plan exchange, the first
+move applied to u_old (cmpc_iterate with CMPC_APPLY_MOVE: SURVEY §8(a)
+a1-a13).  QP solves per step = B * S * K per GPU.
 
 Inputs are resident in HBM before the timed region: NB distinct synthetic
 batches are uploaded once and step i binds batch i % NB,
@@ -15,11 +16,15 @@ persist, as in the reference's closed loop.
 
 Multi-GPU: one process per GPU (torch.distributed.run), scenarios sharded
 across ranks with no data-path collective (weak scaling); the barrier and
-the max-over-ranks of the elapsed time use torch.distributed (RCCL).
+the max-over-ranks of the elapsed time use torch.distributed (RCCL).  The
+`coupled` section beside the metric runs SURVEY config 4 on the same ranks:
+S_local = 8 sub-controllers per GPU of S_total = 8 x world per scenario, the
+plans all-gathered over RCCL once per Jacobi iteration.
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -55,6 +60,14 @@ def iterate_flops(cfg) -> float:
     return 2 * p * ny * m * nuo + 2 * p * ny * nV
 
 
+def applied_iterate_flops(cfg) -> float:
+    """FLOPs one Jacobi iteration of this build performs before the solve:
+    f_k = f + G du_other, G nV x nVo (built once per step in the build
+    kernel)."""
+    nuo = cfg.nu_tot - cfg.nu
+    return 2.0 * cfg.nV * cfg.m * nuo
+
+
 def build_bytes(cfg, L) -> float:
     """Algorithmic HBM bytes of one sub-controller build: its lin record
     (Aorig, Bin, Csel, f, dx_aug, y_prev) + u_old in, the condensed QP out."""
@@ -64,9 +77,67 @@ def build_bytes(cfg, L) -> float:
     return 8.0 * (rec + nu_tot + out)
 
 
-def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
+# sources that determine the build kernel's code (and so its HBM traffic)
+BUILD_SOURCES = ("compressor-mpc_amd/csrc/build_rows.hip", "compressor-mpc_amd/csrc/rows_blocks.inc",
+                 "compressor-mpc_amd/csrc/rows_layout.cpp", "compressor-mpc_amd/csrc/cmpc_internal.h",
+                 "compressor-mpc_amd/csrc/Makefile")
+
+
+def build_source_hash() -> str:
+    """sha256 over the build kernel's sources: ties a PMC traffic figure
+    under profiles/ to the code it was measured on."""
+    h = hashlib.sha256()
+    for rel in BUILD_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(rel.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(B: int, kernel: str):
+    """(bytes per launch, provenance) from profiles/pmc_build_coop_p50.json
+    when it was measured on this batch, this kernel and these sources;
+    (None, reason) otherwise."""
+    path = os.path.join(ROOT, "profiles", "pmc_build_coop_p50.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None, {"file": "profiles/pmc_build_coop_p50.json", "status": "missing"}
+    prov = {"file": "profiles/pmc_build_coop_p50.json", "pmc_source": rec.get("source"),
+            "round": rec.get("round"), "measured_source_hash": rec.get("build_source_hash"),
+            "current_source_hash": build_source_hash()}
+    if rec.get("batch") != B or rec.get("kernel") != kernel:
+        prov["status"] = "not this workload"
+        return None, prov
+    if rec.get("build_source_hash") != prov["current_source_hash"]:
+        prov["status"] = "stale: measured on other build-kernel sources"
+        return None, prov
+    prov["status"] = "measured on these sources (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes)"
+    return rec.get("hbm_bytes_per_launch"), prov
+
+
+def cpu_quota():
+    """CPUs this process may use: affinity mask and cgroup v2 quota."""
+    out = {}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        out["cgroup_cpu_quota"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def cpu_baseline(cfg, arrays, lin, u_old, K, target_s):
     """The oracle (CPU restatement of the reference path: O(p^2) Su loop,
-    dense products, the build's active-set solver) on a bounded sample."""
+    dense products, the build's active-set solver) on a bounded sample of
+    the bench's batch 0, in three legs: one thread; as many threads as the
+    process may run at once (affinity mask and cgroup CPU quota, the value);
+    and os.cpu_count() threads (all host cores) when that is
+    more.  The single-thread leg runs first: idle OpenMP workers of a wide
+    leg spin and eat the quota of whatever runs after them."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     from cmpc._abi import CmpcDims
@@ -85,13 +156,23 @@ def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
             O.step(dims, arrays, lin_s, K, u_s, du_s, ws_s, threads=th)
         return (time.perf_counter() - t0) / reps
 
-    probe = min(64, lin.shape[0] // S)
-    t1 = run(probe, threads, 1)
-    nb = int(min(lin.shape[0] // S, max(probe, probe * target_s / max(t1, 1e-6))))
-    t_pass = run(nb, threads, 1)
-    reps = max(1, int(round(target_s / max(t_pass, 1e-6))))
-    dt = run(nb, threads, reps)
-    t_single = run(probe, 1, 1)
+    def leg(threads, seconds):
+        probe = min(64, lin.shape[0] // S)
+        t1 = run(probe, threads, 1)
+        nb = int(min(lin.shape[0] // S, max(probe, probe * seconds / max(t1, 1e-6))))
+        t_pass = run(nb, threads, 1)
+        reps = max(1, int(round(seconds / max(t_pass, 1e-6))))
+        dt = run(nb, threads, reps)
+        return {"value": nb * S * K / dt, "threads": threads, "scenarios": nb, "steps": reps,
+                "seconds": dt * reps, "us_per_scenario_step": dt / nb * 1e6}
+
+    share = cpu_quota()
+    host = os.cpu_count() or 1
+    usable = min([host] + [int(v) for v in (share.get("affinity_cpus"), share.get("cgroup_cpu_quota"))
+                           if v])
+    single = leg(1, min(5.0, target_s / 2))
+    main_leg = leg(usable, target_s)
+    all_leg = leg(host, target_s / 2) if host > usable else None
     model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -99,18 +180,22 @@ def cpu_baseline(cfg, arrays, lin, u_old, K, target_s, threads):
     except OSError:
         pass
     return {
-        "value": nb * S * K / dt,
-        "cpu_model": model,
-        "host_cpus": os.cpu_count(),
-        "seconds": dt * reps,
+        "value": main_leg["value"],
         "unit": "QP solves/s",
-        "cores": threads,
+        "cores": usable,
         "kind": "port",
-        "sample": (f"{reps} control steps of {nb} scenarios x {S} sub-controllers x K={K} "
-                   f"Jacobi iterations (build + solves) of batch 0, oracle/liboracle.so "
-                   f"(reference op order, -O3, OpenMP), {dt * reps:.1f} s"),
-        "single_thread_value": probe * S * K / t_single,
-        "single_thread_us_per_scenario_step": t_single / probe * 1e6,
+        "cpu_model": model,
+        "host_cpus": host,
+        "cpu_share": share,
+        "sample": (f"{main_leg['steps']} control steps of {main_leg['scenarios']} scenarios x {S} "
+                   f"sub-controllers x K={K} Jacobi iterations (build + solves) of batch 0, "
+                   f"oracle/liboracle.so (reference op order, -O3, OpenMP over scenarios, {usable} "
+                   f"threads), {main_leg['seconds']:.1f} s"),
+        "single_thread": single,
+        "all_host_cpus": all_leg,
+        "threads_note": ("value: as many OpenMP threads as the process may run at once (the smaller "
+                         "of the affinity mask and the cgroup CPU quota); all_host_cpus: "
+                         "os.cpu_count() threads as BASELINE.md §2 asks, which the quota time-slices"),
         "reference_recorded": {
             "note": "context, not comparison (BASELINE.md §1): the reference's own per-step wall "
                     "times from results/parallel/run*/coop{1,9}.dat, p = 100, one thread, CPU unrecorded",
@@ -134,6 +219,8 @@ def main():
                          "passed: the chip ramps its clock over the first ~40 ms of this load "
                          "(tools/time_clock_ramp.py), and the metric is the steady state")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
+    ap.add_argument("--coupled-batch", type=int, default=4096, help="config-4 scenarios per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for the barrier and the max over ranks "
                          "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -202,12 +289,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     # the roofline kernel (build) carries dispatch-stamped HIP events in the
-    # timed steps; the iterate kernel is timed in its own pass afterwards
+    # timed steps; the iterate kernel is timed in its own pass afterwards.
+    # The timed steps apply the first move (UpdateUOld):
+    # u_old moves from the batch's drawn state over the K timed steps (the
+    # warmup and settle steps leave it unchanged) and is restored after.
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
     for i in range(args.steps):
         ctx.bind_lin(batches[(first + i) % NB].data_ptr())
-        ctx.step(K, 0)
+        ctx.step(K, cmpc.CMPC_APPLY_MOVE)
     ctx.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
@@ -221,17 +311,20 @@ def main():
     elapsed_max = float(t.item())
 
     du, st, nw = ctx.download()
-    _, _, ws_now = ctx.get_state()
+    u_moved, _, ws_now = ctx.get_state()
+    u_drift = float(np.abs(u_moved - u_old).max())
 
     # the iterate kernel's own time: the same step loop, events on the iterate
     # only (after the headline measurement, untimed for `value`)
+    ctx.set_state(u_old, None, None)
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
     for i in range(args.steps):
         ctx.bind_lin(batches[(first + args.steps + i) % NB].data_ptr())
-        ctx.step(K, 0)
+        ctx.step(K, cmpc.CMPC_APPLY_MOVE)
     ctx.synchronize()
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     ctx.enable_timing(False)
+    ctx.set_state(u_old, None, None)
 
     def warm():
         """Build launches on a resident batch for --settle-seconds, then the
@@ -425,6 +518,32 @@ def main():
                         "one scenario, p = 100) is 900.4 us"}
         except Exception as e:  # reported, never required
             log(f"closed loop with the plant failed: {e}")
+    # SURVEY config 4 (sub-controllers sharded over the ranks, RCCL all-gather
+    # of the plans once per Jacobi iteration), beside the metric: every rank
+    # takes part, so at world N it times the exchange over xGMI
+    coupled = None
+    if not args.no_coupled:
+        from cmpc.coupled import run_coupled_bench
+        rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
+                               steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds)
+        tc = torch.tensor([rc["elapsed_s"]], dtype=torch.float64,
+                          device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
+        if dist:
+            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        el_c = float(tc.item())
+        coupled = dict(rc)
+        coupled.pop("elapsed_s")
+        coupled.update({
+            "qp_solves_per_s": world * rc["qp_per_gpu"] * K * rc["steps"] / el_c,
+            "ms_per_step": el_c / rc["steps"] * 1e3,
+            "exchange": ("RCCL all_gather_into_tensor of B x S_local x nV plans per Jacobi iteration "
+                         f"({args.dist_backend})" if world > 1 else "local copy (world size 1)"),
+            "note": "SURVEY config 4: S_total = 8 x world sub-controllers per scenario (synthetic "
+                    "coupling, cmpc/coupled.py), 8 per GPU; step = build + K x (all-gather + "
+                    "coupled iteration), first move applied; per-GPU work grows with S_total "
+                    "(G_ext is nV x (S_total - 1) nV per QP); gather_ms from events in a "
+                    "separate pass"})
+
     ok_frac = float((st == 0).mean())
     active_frac = float((ws_now != 0).mean())
     mean_chg = float(nw.mean())
@@ -435,17 +554,9 @@ def main():
     avg_build_s = build_ms / max(n_build, 1) / 1e3
     f_build = build_flops(cfg, L.naug, L.nd)
     achieved_tf = B * S * f_build / avg_build_s / 1e12
-    traffic = None
     build_kernel = ("cmpc_build_rows_kernel" if ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS
                     else "cmpc_build_kernel")
-    pmc = os.path.join(ROOT, "profiles", "pmc_build_coop_p50.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc))
-            if rec.get("batch") == B and rec.get("kernel") == build_kernel:
-                traffic = rec.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_prov = pmc_traffic(B, build_kernel)
 
     out = {
         "metric": "QP solves/sec (whole node), cooperative-parallel MPC, horizon p=50",
@@ -480,24 +591,29 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved_tf / FP64_PEAK_TFLOPS,
             "traffic": traffic,
+            "traffic_provenance": traffic_prov,
             "flops_per_qp": f_build,
             "algorithmic_bytes_per_qp": build_bytes(cfg, L),
             "avg_launch_ms": avg_build_s * 1e3,
             "launches": n_build,
         },
-        "step_roofline": {
-            "definition": ("SURVEY.md 8(d) path roofline: (F_build + K F_it) algorithmic FLOPs per "
-                           "sub-controller x B*S per GPU / measured step time (max over ranks), "
-                           "against the FP64 peak"),
-            "flops_per_qp_step": f_build + K * iterate_flops(cfg),
-            "achieved": B * S * (f_build + K * iterate_flops(cfg)) / (elapsed_max / args.steps) / 1e12,
+        "path_roofline": {
+            "definition": ("whole step against the FP64 peak: the FLOPs this build performs per "
+                           "sub-controller step that the reference's path also needs (F_build of "
+                           "SURVEY 8(d), plus 2 nV nVo per Jacobi iteration for f_k = f + G du_other) "
+                           "x B*S per GPU / measured step time (max over ranks); the QP solves "
+                           "themselves are not counted"),
+            "flops_per_qp_step": f_build + K * applied_iterate_flops(cfg),
+            "achieved": B * S * (f_build + K * applied_iterate_flops(cfg)) / (elapsed_max / args.steps)
+                        / 1e12,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s per GPU",
-            "frac": B * S * (f_build + K * iterate_flops(cfg)) / (elapsed_max / args.steps) / 1e12
-                    / FP64_PEAK_TFLOPS,
-            "note": ("F_it counts the reference's per-iteration ApplyOtherInput products; this build "
-                     "forms G = Su'W Su_other once in the build kernel (2 p ny nV nVo FLOPs per QP, "
-                     "not in F_build) and applies it with nV nVo FMAs per iteration"),
+            "frac": B * S * (f_build + K * applied_iterate_flops(cfg)) / (elapsed_max / args.steps)
+                    / 1e12 / FP64_PEAK_TFLOPS,
+            "note": ("SURVEY 8(d)'s F_it (the reference's (p ny)-long ApplyOtherInput products, "
+                     f"{iterate_flops(cfg):.0f} FLOPs per iteration) is not credited: this build "
+                     "forms G = Su'W Su_other once in the build kernel and applies it with nV nVo "
+                     "FMAs per iteration"),
         },
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1),
@@ -506,13 +622,14 @@ def main():
         "k1": k1,
         "qp_status_ok_fraction": ok_frac,
         "qp_active_constraint_fraction": active_frac,
+        "u_old_max_drift_over_timed_steps": u_drift,
         "mean_working_set_changes_last_solve": mean_chg,
         "closed_loop_device_resident": closed,
+        "coupled": coupled,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(cfg, arrays, lin0, u_old, K, args.cpu_seconds, threads)
+            out["cpu_baseline"] = cpu_baseline(cfg, arrays, lin0, u_old, K, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu baseline failed: {e}")
             out["cpu_baseline"] = None

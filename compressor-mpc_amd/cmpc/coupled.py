@@ -121,3 +121,74 @@ class CoupledRank:
         for k in range(K):
             self.gather()
             self.iterate(k == K - 1)
+
+
+def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: int = 4096, p: int = 50,
+                      K: int = 9, steps: int = 20, warmup: int = 3, settle_seconds: float = 0.25,
+                      S_total: int = 0, group=None) -> dict:
+    """SURVEY config 4 on this rank: B scenarios x S_local sub-controllers
+    (global indices rank * S_local + i of S_total = S_local * world), one
+    step = build + K x (all-gather of the plans, coupled Jacobi iteration),
+    the first move applied in the last iteration.  The caller has set up the
+    process group (nccl = RCCL over xGMI between GPUs) when world > 1.
+    Returns this rank's timings; the whole-job value needs the max over ranks
+    of `elapsed_s` (the caller's barrier + all-reduce)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from . import Context, controller_arrays, reference_config
+    from .configs import reference_setup
+    from .synthetic import synthetic_batch
+
+    S_total = S_total or S_local * world
+    cfg = reference_config("par", "coop", p=p)
+    arr = controller_arrays(cfg, reference_setup("par", "coop"))
+    nqp = B * S_local
+    lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=500 + rank, n_distinct=1024)
+    ctx = Context(cfg, nqp // cfg.S, device=device)
+    try:
+        ctx.configure(arr)
+        ctx.set_state(u_old, np.zeros((nqp, cfg.nV)), np.zeros(nqp, np.uint32))
+        ctx.upload_lin(lin)
+        ctx.build()
+        ctx.init_warmstart()
+        _, _, G = ctx.download_qp()
+        G_ext = torch.from_numpy(synthetic_g_ext(G, S_total, S_local, rank * S_local)).to(f"cuda:{device}")
+        cr = CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group)
+        for _ in range(warmup):
+            cr.step(K)
+        torch.cuda.synchronize(device)
+        t_end = time.perf_counter() + settle_seconds
+        while time.perf_counter() < t_end:
+            cr.step(K)
+            torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier(group=group)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            cr.step(K)
+        torch.cuda.synchronize(device)
+        elapsed = time.perf_counter() - t0
+        # the exchange alone: events around the gathers of a second pass
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(K)]
+        ctx.build()
+        for k in range(K):
+            ev[k][0].record()
+            cr.gather()
+            ev[k][1].record()
+            cr.iterate(k == K - 1)
+        torch.cuda.synchronize(device)
+        gather_ms = sum(a.elapsed_time(b) for a, b in ev) / K
+        _, st, _ = ctx.download()
+        return {"elapsed_s": elapsed, "steps": steps, "qp_per_gpu": nqp, "S_total": S_total,
+                "S_local": S_local, "B": B, "p": p, "K": K,
+                "G_ext_MB_per_gpu": G_ext.numel() * 8 / 1e6,
+                "gather_ms_per_iteration": gather_ms,
+                "gather_bytes_per_iteration": world * nqp * cfg.nV * 8,
+                "qp_status_ok_fraction": float((st == 0).mean())}
+    finally:
+        ctx.close()

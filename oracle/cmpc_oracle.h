@@ -84,6 +84,7 @@ typedef struct or_qp_info {
   uint32_t ws;     /* working set on exit */
   int32_t ntrace;
   uint8_t trace[16];
+  double margin;   /* smallest relative decision margin (checker only; or_qp.c header) */
 } or_qp_info;
 
 /* min 1/2 x'Hx + g'x  s.t. lb <= x <= ub, lbA <= A x <= ubA with the
@@ -113,7 +114,7 @@ typedef struct or_cfg {
 int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
             uint32_t flags, int init, int threads, double* u_old,
             double* du_old, uint32_t* ws, double* du, int32_t* status,
-            int32_t* nwsr, uint8_t* trace, int32_t* ntrace);
+            int32_t* nwsr, uint8_t* trace, int32_t* ntrace, double* margin);
 
 /* ---- plant simulation (or_plant.c, or_sim.c) ---- */
 /* GetDerivative of the plant (parallel_compressors.cc:9-26, serial_compressors.cc:8-26). */

@@ -16,10 +16,14 @@
  *   UpdateUOld / SendUHelper (own inputs of    include/nerve_center.h:313-328,
  *     each sub-controller += first move)      include/distributed_controller.h:146-152
  *
+ * margin (optional, B*S): per QP slot the smallest decision margin of its
+ * solves in this step (or_qp_info.margin), the checker's near-tie flag.
+ *
  * Other-controller plans are laid out in Su_other's move-major column order
  * (du_other[mv*nuo + rank*nu + c]); for S = 2 this is exactly the
  * reference's concatenation (nerve_center.h:283-285 vs aug_lin_sys.cc:325-327).
  */
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -31,7 +35,7 @@
 int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
             uint32_t flags, int init, int threads, double* u_old,
             double* du_old, uint32_t* ws, double* du, int32_t* status,
-            int32_t* nwsr, uint8_t* trace, int32_t* ntrace) {
+            int32_t* nwsr, uint8_t* trace, int32_t* ntrace, double* margin) {
   cmpc_layout L;
   if (or_layout_of(d, &L)) return -1;
   const int S = d->S, B = d->B, nu = d->nu, nu_tot = d->nu_tot, m = d->m;
@@ -59,6 +63,8 @@ int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
                   NULL);
     }
     double lb[CMPC_MAX_NV], ub[CMPC_MAX_NV], lbA[CMPC_MAX_NV], ubA[CMPC_MAX_NV];
+    if (margin)
+      for (int s = 0; s < S; ++s) margin[(size_t)b * S + s] = HUGE_VAL;
     if (init) {
       for (int s = 0; s < S; ++s) {
         const size_t q = (size_t)b * S + s;
@@ -74,6 +80,7 @@ int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
         or_qp_solve(nV, nu, H + s * nV * nV, f + s * nV, lb, ub, lbA, ubA, 0u,
                     CMPC_NWSR_MAX, xs, &info);
         ws[q] = info.ws;
+        if (margin && info.margin < margin[q]) margin[q] = info.margin;
       }
     }
     for (int s = 0; s < S; ++s)
@@ -121,6 +128,7 @@ int or_step(const cmpc_dims* d, const or_cfg* cfg, const double* lin, int K,
         nwsr[q] = info.nchg;
         if (trace) memcpy(trace + (q * K + k) * 16, info.trace, 16);
         if (ntrace) ntrace[q * K + k] = info.ntrace;
+        if (margin && info.margin < margin[q]) margin[q] = info.margin;
       }
       memcpy(dprev, dnew, sizeof(double) * S * nV);
     }

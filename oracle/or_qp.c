@@ -32,6 +32,27 @@
  *      u_p += t; full step adds p, partial step drops the blocker.
  *   Every add/drop counts one change; the 11th change -> MAX_NWSR.
  *   On success, variables at an active bound are set exactly to that bound.
+ *
+ * Decision margins (info->margin; the checker's near-tie flag, not part of
+ * the algorithm): every comparison that picks a branch or an index above
+ * also records how far its two sides were apart, relative to the scale of
+ * the compared quantities, and info->margin is the smallest such distance
+ * over the whole solve:
+ *   multipliers  lam_a vs -tol_d and vs the chosen most negative one,
+ *                scale S_lam = max(|g|_inf, (1 + max|H_ii|) S_x, tol_d)
+ *   slacks       slack vs -TOL_P(1 + |beta|) and vs the chosen most violated
+ *                one, scale S_x = max of the finite |bounds| and |x_u|_inf
+ *   step ratios  lam_a / r_a vs the chosen t1 (cross-multiplied:
+ *                lam_a r_k - lam_k r_a over S_lam max(r_a, r_k)); r_a vs TOL_R
+ *                over max(1, |r_a|)
+ *   dependence   nu_p'z vs TOL_Z nu_p'Hinv nu_p over nu_p'Hinv nu_p
+ *   step kind    t2 vs t1 over max(|t1|, |t2|)
+ *   factor       working-set LDL' pivots over the diagonal of M
+ * (tests against a tolerance skip a rounding-noise zero: see mg_tol).
+ * A QP whose inputs differ from another's by FP64 reassociation only
+ * (~1e-13 relative) takes the same decisions whenever its margin is well
+ * above that; tests allow differing working-set sequences only where the
+ * margin is below 1e-9 (tests/test_solver_margins.py).
  * Working-set word: bit j = constraint j active (j < n: bound on x_j,
  * j >= n: rate row j - n), bit 16 + j = at its upper side.
  */
@@ -50,15 +71,35 @@ typedef struct {
   int n, nu;
   double Hinv[QMAX][QMAX];
   const double *lb, *ub, *lbA, *ubA;
+  double s_x, s_lam; /* margin scales */
+  double margin;     /* smallest relative decision margin so far */
 } qp_t;
+
+/* record |a - b| / scale as a decision margin */
+static void mg(qp_t* q, double a, double b, double scale) {
+  const double v = fabs(a - b) / (scale > 0 ? scale : 1e-300);
+  if (v < q->margin) q->margin = v;
+}
+
+/* the same for a test of a against a tolerance thr, |thr| = 1e-12 of the
+ * scale (or more).  A value within 1e-3 |thr| of zero is a mathematical zero
+ * evaluated with rounding noise: a dependent constraint normal (nu_p'z with
+ * nu_p in the span of the active normals), a structural zero of H or of the
+ * normals, a constraint that x satisfies with equality by construction.
+ * Such a value is zero for any perturbation of H and g, and its noise
+ * (~1e-16 of the scale, far under 1e-3 |thr|) cannot carry it across thr on
+ * any evaluation order, so it records no margin. */
+static void mg_tol(qp_t* q, double a, double thr, double scale) {
+  if (fabs(a) > 1e-3 * fabs(thr)) mg(q, a, thr, scale);
+}
 
 static int ldl(int n, double M[QMAX][QMAX], double L[QMAX][QMAX],
                double D[QMAX]) {
   for (int j = 0; j < n; ++j) {
     double d = M[j][j];
     for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
-    if (!(d > 0)) return -1;
     D[j] = d;
+    if (!(d > 0)) return -(j + 1);
     L[j][j] = 1.0;
     for (int i = j + 1; i < n; ++i) {
       double s = M[i][j];
@@ -125,7 +166,7 @@ typedef struct {
 } wset_t;
 
 /* (re)build h, M = N'Hinv N and its LDL' for the current W */
-static int wset_factor(const qp_t* q, wset_t* W) {
+static int wset_factor(qp_t* q, wset_t* W) {
   double M[QMAX][QMAX];
   for (int a = 0; a < W->K; ++a) hinv_nu(q, W->j[a], W->side[a], W->h[a]);
   for (int a = 0; a < W->K; ++a)
@@ -134,7 +175,12 @@ static int wset_factor(const qp_t* q, wset_t* W) {
       M[a][b] = v;
       M[b][a] = v;
     }
-  return ldl(W->K, M, W->L, W->D);
+  const int rc = ldl(W->K, M, W->L, W->D);
+  /* margin of the pivot test d > 0 (pivots relative to M's diagonal), up
+   * to and including a failing pivot */
+  const int np = rc ? -rc : W->K;
+  for (int a = 0; a < np; ++a) mg(q, W->D[a], 0.0, fabs(M[a][a]));
+  return rc;
 }
 
 static void wset_drop(wset_t* W, int a) {
@@ -174,6 +220,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
   double x[QMAX], xu[QMAX];
   memset(info, 0, sizeof *info);
   memset(info->trace, 0xFF, sizeof info->trace);
+  q.margin = HUGE_VAL;
   q.n = n;
   q.nu = nu;
   q.lb = lb; q.ub = ub; q.lbA = lbA; q.ubA = ubA;
@@ -184,7 +231,9 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     double Hm[QMAX][QMAX], L[QMAX][QMAX], D[QMAX];
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) Hm[i][j] = H[i * n + j];
-    if (ldl(n, Hm, L, D)) {
+    const int rc = ldl(n, Hm, L, D);
+    for (int a = 0; a < (rc ? -rc : n); ++a) mg(&q, D[a], 0.0, fabs(H[a * n + a]));
+    if (rc) {
       status = CMPC_QP_NOT_PD;
       goto done;
     }
@@ -206,6 +255,17 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
   for (int i = 0; i < n; ++i)
     if (fabs(H[i * n + i]) > hmax) hmax = fabs(H[i * n + i]);
   const double tol_d = TOL_D * (1.0 + hmax);
+  {
+    double sx = 0, sg = 0;
+    for (int i = 0; i < n; ++i) {
+      const double v[5] = {lb[i], ub[i], lbA[i], ubA[i], xu[i]};
+      for (int k = 0; k < 5; ++k)
+        if (isfinite(v[k]) && fabs(v[k]) > sx) sx = fabs(v[k]);
+      if (fabs(g[i]) > sg) sg = fabs(g[i]);
+    }
+    q.s_x = sx;
+    q.s_lam = fmax(fmax(sg, (1.0 + hmax) * sx), tol_d);
+  }
 
   /* A. warm start from ws_in */
   for (int j = 0; j < 2 * n; ++j)
@@ -227,6 +287,10 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
         wv = W.lam[a];
         worst = a;
       }
+    for (int a = 0; a < W.K; ++a) {
+      mg_tol(&q, W.lam[a], -tol_d, q.s_lam);
+      if (worst >= 0 && a != worst && W.lam[a] < -tol_d) mg(&q, W.lam[a], wv, q.s_lam);
+    }
     if (worst < 0) break;
     trace_push(info, 0, W.j[worst], W.side[worst]);
     wset_drop(&W, worst);
@@ -252,6 +316,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
       for (int s = 0; s < 2; ++s) {
         const double b = beta(&q, j, s);
         const double sl = nu_dot(&q, j, s, x) - b;
+        mg_tol(&q, sl, -TOL_P * (1.0 + fabs(b)), q.s_x);
         if (sl < -TOL_P * (1.0 + fabs(b)) && (pj < 0 || sl < pv)) {
           pj = j;
           ps = s;
@@ -259,6 +324,15 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
         }
       }
     }
+    if (pj >= 0) /* the most violated against the other violated ones */
+      for (int j = 0; j < 2 * n; ++j) {
+        if (act & (1u << j)) continue;
+        for (int s = 0; s < 2; ++s) {
+          const double b = beta(&q, j, s);
+          const double sl = nu_dot(&q, j, s, x) - b;
+          if (sl < -TOL_P * (1.0 + fabs(b)) && !(j == pj && s == ps)) mg(&q, sl, pv, q.s_x);
+        }
+      }
     if (pj < 0) break; /* optimal */
     double up = 0.0;
     for (;;) {
@@ -283,6 +357,12 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
             k = a;
           }
         }
+      for (int a = 0; a < W.K; ++a) {
+        mg_tol(&q, rv[a], TOL_R, fmax(1.0, fabs(rv[a])));
+        if (k >= 0 && a != k && rv[a] > TOL_R) /* blocking ratio vs the chosen one */
+          mg(&q, W.lam[a] * rv[k], W.lam[k] * rv[a], q.s_lam * fmax(rv[a], rv[k]));
+      }
+      mg_tol(&q, zn, TOL_Z * den, fabs(den));
       if (zn <= TOL_Z * den) { /* nu_p dependent on the active normals */
         if (k < 0) {
           status = CMPC_QP_INFEASIBLE;
@@ -301,6 +381,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
       }
       const double sl = nu_dot(&q, pj, ps, x) - beta(&q, pj, ps);
       const double t2 = -sl / zn;
+      if (k >= 0) mg(&q, t2, t1, fmax(fabs(t1), fabs(t2)));
       const int full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
       for (int r = 0; r < n; ++r) x[r] = x[r] + t * z[r];
@@ -328,6 +409,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
 done:
   info->status = status;
   info->nchg = chg;
+  info->margin = q.margin;
   {
     uint32_t w = 0;
     for (int a = 0; a < W.K; ++a)

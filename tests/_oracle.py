@@ -22,7 +22,7 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 class OrQpInfo(ctypes.Structure):
     _fields_ = [("status", ctypes.c_int32), ("nchg", ctypes.c_int32),
                 ("ws", ctypes.c_uint32), ("ntrace", ctypes.c_int32),
-                ("trace", ctypes.c_uint8 * 16)]
+                ("trace", ctypes.c_uint8 * 16), ("margin", ctypes.c_double)]
 
 
 class OrCfg(ctypes.Structure):
@@ -57,7 +57,7 @@ def lib():
                                   P(d), u32, ctypes.c_int, P(d), P(OrQpInfo)]
         L.or_step.argtypes = [P(CmpcDims), P(OrCfg), P(d), ctypes.c_int, u32, ctypes.c_int,
                               ctypes.c_int, P(d), P(d), P(u32), P(d), P(i32), P(i32),
-                              P(ctypes.c_uint8), P(i32)]
+                              P(ctypes.c_uint8), P(i32), P(d)]
         _lib = L
     return _lib
 
@@ -129,8 +129,10 @@ def qp_solve(H, g, lb, ub, lbA, ubA, nu, ws_in=0, max_chg=10):
 
 
 def step(dims, arrays, lin, K, u_old, du_old, ws, flags=0, init=False, threads=1,
-         want_trace=False):
-    """Batched oracle step; state arrays are updated in place."""
+         want_trace=False, margin=None):
+    """Batched oracle step; state arrays are updated in place.  margin: an
+    optional (B*S,) float64 array that receives each QP slot's smallest
+    decision margin over the step's solves (or_qp.c)."""
     L = layout(dims)
     nq = dims.B * dims.S
     du = np.zeros((nq, L.nV)); status = np.zeros(nq, np.int32); nwsr = np.zeros(nq, np.int32)
@@ -143,7 +145,8 @@ def step(dims, arrays, lin, K, u_old, du_old, ws, flags=0, init=False, threads=1
     rc = lib().or_step(ctypes.byref(dims), ctypes.byref(cfg), dptr(lin), K, flags, int(init),
                        threads, dptr(u_old), dptr(du_old), uptr(ws), dptr(du), iptr(status),
                        iptr(nwsr), bptr(trace) if want_trace else None,
-                       iptr(ntrace) if want_trace else None)
+                       iptr(ntrace) if want_trace else None,
+                       dptr(margin) if margin is not None else None)
     assert rc == 0
     return du, status, nwsr, trace, ntrace
 

@@ -217,3 +217,78 @@ def test_gpu_coupled_two_ranks_equal_one():
     sl = S_TOTAL // world
     got = got.reshape(world, B, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
     assert np.array_equal(got, one)
+
+
+@pytest.mark.gpu
+def test_gpu_config4_full_size_matches_oracle():
+    """SURVEY config 4 at its real size on one GPU: 64 sub-controllers per
+    scenario (p = 50 coop QPs, synthetic coupling), 4 096 scenarios
+    (262 144 QPs, 2.1 GB of G_ext), K = 9 Jacobi iterations through
+    CoupledRank (world size 1).  Every QP's status over the whole batch,
+    and 16 whole scenarios (1 024 QPs) bit-exact against the oracle's loop
+    on the product's own QPs (same f_k summation order, or_qp_solve)."""
+    import torch
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.coupled import CoupledRank
+    from cmpc.synthetic import synthetic_batch
+    S_total, Bsc, K4 = 64, 4096, 9
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    nqp = Bsc * S_total
+    lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=64, n_distinct=1024)
+    ctx = cmpc.Context(cfg, nqp // cfg.S, device=0)
+    try:
+        ctx.configure(arr)
+        ctx.set_state(u_old, np.zeros((nqp, cfg.nV)), np.zeros(nqp, np.uint32))
+        ctx.upload_lin(lin)
+        ctx.build()
+        H, f, G = ctx.download_qp()
+        Gx_host = synthetic_g_ext(G, S_total, S_total, 0)           # (4 * 63 * 4, nqp)
+        Gx = torch.from_numpy(Gx_host).cuda()
+        cr = CoupledRank(ctx, S_total, S_total, 0, 1, Gx)
+        cr.step(K4)
+        torch.cuda.synchronize()
+        du_gpu = cr.du_local.cpu().numpy()
+        _, st, nw = ctx.download()
+        _, _, ws_gpu = ctx.get_state()
+    finally:
+        ctx.close()
+    print("config 4: QPs", nqp, "status OK", (st == 0).mean(), "with active constraints",
+          (ws_gpu != 0).mean())
+    assert (st == 0).mean() > 0.999
+    # 16 whole scenarios through the oracle's loop (vectorised over the
+    # sample's QPs, the kernel's summation order j, then a, then v)
+    sample = np.linspace(0, Bsc - 1, 16).astype(int)
+    qs = (sample[:, None] * S_total + np.arange(S_total)[None, :]).reshape(-1)
+    G3 = Gx_host.reshape(4, (S_total - 1) * 4, nqp)[:, :, qs]      # (4, 252, nq_s)
+    nu = cfg.nu
+    ws = np.zeros(len(qs), np.uint32)
+    st_o = np.zeros(len(qs), np.int32)
+    prev = np.zeros((len(sample), S_total, 4))
+    for k in range(K4):
+        fk = f[qs].copy()
+        for s in range(S_total):
+            rows = np.arange(len(sample)) * S_total + s
+            jj = 0
+            for j in range(S_total):
+                if j == s:
+                    continue
+                for a in range(4):
+                    for v in range(4):
+                        fk[rows, a] = fk[rows, a] + G3[a, jj * 4 + v, rows] * prev[:, j, v]
+                jj += 1
+        new = np.zeros_like(prev)
+        for i, q in enumerate(qs):
+            s_cfg = q % cfg.S
+            lo = np.tile(arr.lower[s_cfg] - u_old[q, :nu], 2)
+            up = np.tile(arr.upper[s_cfg] - u_old[q, :nu], 2)
+            x, info = O.qp_solve(H[q], fk[i], lo, up, np.tile(arr.rate_lower[s_cfg], 2),
+                                 np.tile(arr.rate_upper[s_cfg], 2), nu, int(ws[i]))
+            ws[i] = info.ws
+            st_o[i] = info.status
+            new[i // S_total, i % S_total] = x
+        prev = new
+    assert np.array_equal(st[qs], st_o)
+    assert np.array_equal(ws_gpu[qs], ws)
+    assert np.array_equal(du_gpu[qs], prev.reshape(-1, 4))

@@ -7,9 +7,12 @@ Tolerances:
               propagation and never forms Su; the oracle follows the
               reference's O(p^2) order)
   du        : abs 1e-10 + rel 1e-9
-  active-set: working-set change sequences bit-exact, except QPs flagged as
-              near-degenerate (a decision within 1e-9 of a tie), which are
-              counted and bounded
+  active-set: statuses, nWSR, working sets and working-set change sequences
+              bit-exact, except scenarios whose oracle solves take a
+              decision within 1e-9 (relative) of a tie (the oracle's decision
+              margin, oracle/or_qp.c; tests/test_solver_margins.py shows it
+              predicts where sequences can diverge); flagged scenarios are
+              counted and printed, nothing else is excused
   solver    : on identical (H, g, bounds, ws) the device solver is bit-exact
               with the oracle solver (same arithmetic order, no contraction)
 """
@@ -200,11 +203,38 @@ STEP_CASES = [("par", "coop", 20, 9), ("par", "coop", 50, 9), ("par", "ncoop", 5
               ("par", "cent", 50, 1), ("ser", "ncoop", 50, 9),
               ("ser", "coop", 50, 9), ("ser", "cent", 50, 1)]
 
+NEAR_TIE = 1e-9   # oracle decision margin below which a sequence may differ (or_qp.c)
+
+
+def compare_step(B, S, K, dev, orc, margin, excused):
+    """One step's device results against the oracle's, per scenario.  dev /
+    orc = (du, status, nwsr, ws, trace, ntrace).  Returns (unflagged,
+    flagged) scenario masks of differing working-set sequences; a scenario
+    may differ only when the oracle flags one of its solves as a near-tie
+    (margin < NEAR_TIE) in this step, or it already diverged at a flagged
+    near-tie earlier (its warm starts then differ)."""
+    du, st, nw, ws, tr, ntr = dev
+    odu, ost, onw, ows, otr, ontr = orc
+    seq = np.zeros(B * S, bool)
+    for k in range(K):
+        n_ = ntr[:, k]
+        seq |= n_ != ontr[:, k]
+        for c in range(16):
+            live = c < np.minimum(n_, ontr[:, k])
+            seq |= live & (tr[:, k, c] != otr[:, k, c])
+    diff = ((st != ost) | (nw != onw) | (ws != ows) | seq).reshape(B, S).any(1)
+    flag = (margin < NEAR_TIE).reshape(B, S).any(1)
+    return diff & ~flag & ~excused, diff & (flag | excused)
+
 
 @pytest.mark.parametrize("plant,ctype,p,K", STEP_CASES)
 def test_gpu_step_matches_oracle(plant, ctype, p, K):
     """Three closed-loop steps (state persists: ws, du_old, u_old with the
-    first move applied): plans, statuses, working sets and change sequences."""
+    first move applied), device and oracle each on their own state: plans
+    within tolerance, statuses, nWSR, working sets and the working-set change
+    sequences of every Jacobi iteration bit-exact, except scenarios the
+    oracle flags as near-ties (decision margin < 1e-9, or_qp.c), which are
+    counted and printed."""
     _, setup, _, _ = setup_for(plant, ctype)
     cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
@@ -213,7 +243,7 @@ def test_gpu_step_matches_oracle(plant, ctype, p, K):
     o_u, o_du, o_ws = u_old.copy(), du_old.copy(), ws.copy()
     dims = CmpcDims.from_config(cfg, B)
     nq = B * cfg.S
-    near_tie = 0
+    excused = np.zeros(B, bool)
     with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
         for step in range(3):
             flags = cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE
@@ -226,26 +256,65 @@ def test_gpu_step_matches_oracle(plant, ctype, p, K):
             du, st, nw = ctx.download()
             tr, ntr = ctx.download_trace(K)
             u_g, du_g, ws_g = ctx.get_state()
+            margin = np.zeros(nq)
             odu, ost, onw, otr, ontr = O.step(dims, arr, lin, K, o_u, o_du, o_ws,
                                               flags=cmpc.CMPC_APPLY_MOVE, init=(step == 0),
-                                              want_trace=True)
-            np.testing.assert_allclose(du, odu, rtol=1e-9, atol=1e-10)
-            np.testing.assert_allclose(u_g, o_u, rtol=1e-9, atol=1e-10)
-            mism = np.nonzero((st != ost) | (ws_g != o_ws) | (nw != onw) |
-                              np.any(ntr != ontr, axis=1))[0]
-            near_tie += len(mism)
-            assert len(mism) <= max(1, nq // 100), (step, mism[:10])
-            same = np.ones(nq, bool)
-            same[mism] = False
-            for q in np.nonzero(same)[0]:
-                for k in range(K):
-                    n_ = ntr[q, k]
-                    assert bytes(tr[q, k, :n_]) == bytes(otr[q, k, :n_])
-            # keep the oracle's state in lock-step with the device where they agree
-            o_u[:] = u_g
-            o_du[:] = du_g
-            o_ws[:] = ws_g
-    assert near_tie <= max(1, 3 * nq // 100)
+                                              want_trace=True, margin=margin)
+            bad, flagged = compare_step(B, cfg.S, K, (du, st, nw, ws_g, tr, ntr),
+                                        (odu, ost, onw, o_ws, otr, ontr), margin, excused)
+            print(f"step {step}: scenarios differing at a flagged near-tie {flagged.sum()}, "
+                  f"unflagged {bad.sum()}, smallest oracle margin {margin.min():.3g}")
+            assert not bad.any(), np.flatnonzero(bad)[:10]
+            excused |= flagged
+            keep = np.repeat(~excused, cfg.S)
+            np.testing.assert_allclose(du[keep], odu[keep], rtol=1e-9, atol=1e-10)
+            np.testing.assert_allclose(u_g[keep], o_u[keep], rtol=1e-9, atol=1e-10)
+
+
+def test_gpu_step_matches_oracle_headline_size():
+    """The bench workload (coop-par p = 50, 65 536 scenarios = 131 072 QPs,
+    K = 9): cold solves, then two steps with the first move applied, every
+    QP's status, nWSR, working set and change sequence of every Jacobi
+    iteration against the oracle, each side on its own state."""
+    import os
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B, K = 65536, 9
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=1002, n_distinct=2048)
+    o_u, o_du, o_ws = u_old.copy(), du_old.copy(), ws.copy()
+    dims = CmpcDims.from_config(cfg, B)
+    nq = B * cfg.S
+    threads = min(16, os.cpu_count() or 1)
+    excused = np.zeros(B, bool)
+    active = 0.0
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        for step in range(2):
+            flags = cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE
+            if step == 0:
+                ctx.build()
+                ctx.init_warmstart()
+                ctx.iterate(K, flags)
+            else:
+                ctx.step(K, flags)
+            du, st, nw = ctx.download()
+            tr, ntr = ctx.download_trace(K)
+            u_g, du_g, ws_g = ctx.get_state()
+            margin = np.zeros(nq)
+            odu, ost, onw, otr, ontr = O.step(dims, arr, lin, K, o_u, o_du, o_ws,
+                                              flags=cmpc.CMPC_APPLY_MOVE, init=(step == 0),
+                                              threads=threads, want_trace=True, margin=margin)
+            bad, flagged = compare_step(B, cfg.S, K, (du, st, nw, ws_g, tr, ntr),
+                                        (odu, ost, onw, o_ws, otr, ontr), margin, excused)
+            active = (ws_g != 0).mean()
+            print(f"step {step}: {nq} QPs x {K} iterations, changes {int(ntr.sum())}, active "
+                  f"{active:.3f}; differing at a flagged near-tie {flagged.sum()}, unflagged "
+                  f"{bad.sum()}, QPs flagged {(margin < NEAR_TIE).sum()}")
+            assert not bad.any(), np.flatnonzero(bad)[:10]
+            excused |= flagged
+            keep = np.repeat(~excused, cfg.S)
+            np.testing.assert_allclose(du[keep], odu[keep], rtol=1e-9, atol=1e-10)
+    assert active > 0.05
 
 
 def test_gpu_large_batch_properties():

@@ -69,7 +69,9 @@ def main():
     bk = "cmpc_build_rows_kernel" if "cmpc_build_rows_kernel" in summary["kernels"] else "cmpc_build_kernel"
     b = summary["kernels"].get(bk, {})
     if "hbm_bytes_per_launch" in b:
-        json.dump({"batch": batch, "round": rnd, "kernel": bk,
+        sys.path.insert(0, ROOT)
+        from bench import build_source_hash
+        json.dump({"batch": batch, "round": rnd, "kernel": bk, "build_source_hash": build_source_hash(),
                    "hbm_bytes_per_launch": b["hbm_bytes_per_launch"],
                    "hbm_read_bytes": b["hbm_read_bytes"], "hbm_write_bytes": b["hbm_write_bytes"],
                    "source": f"profiles/{rnd}_pmc.json"},
