@@ -219,6 +219,9 @@ def main():
                          "passed: the chip ramps its clock over the first ~40 ms of this load "
                          "(tools/time_clock_ramp.py), and the metric is the steady state")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the metric's steps (no K = 1, closed-loop, coupled or CPU sections): "
+                         "profiler runs, so that every build launch in the trace is a headline one")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--coupled-batch", type=int, default=4096, help="config-4 scenarios per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -344,185 +347,187 @@ def main():
     # K = 1 (the build-dominated figure beside the K = 9 headline),
     # this rank, after the headline measurement
     k1 = None
-    try:
-        warm()
-        for i in range(2):
-            ctx.bind_lin(batches[i % NB].data_ptr())
-            ctx.step(1, 0)
-        ctx.synchronize()
-        reps1 = max(10, args.steps // 2)
-        t0 = time.perf_counter()
-        for i in range(reps1):
-            ctx.bind_lin(batches[i % NB].data_ptr())
-            ctx.step(1, 0)
-        ctx.synchronize()
-        t_k1 = (time.perf_counter() - t0) / reps1
-        k1 = {"qp_solves_per_s_per_gpu": B * S / t_k1, "ms_per_step": t_k1 * 1e3, "steps": reps1,
-              "note": "K = 1 Jacobi iteration per step (build-dominated), this rank's GPU"}
-    except Exception as e:  # reported, never required
-        log(f"K=1 variant failed: {e}")
-
-    # Closed-loop variant (reported beside the metric, not in `value`): the
-    # records are produced on the device from plant states each step
-    # (cmpc_produce_lin), then build + K iterations with
-    # the first move applied.
-    closed = None
-    try:
-        from cmpc.synthetic import synthetic_operating_points, synthetic_u_old
-        xs, us, ys = synthetic_operating_points(cfg, B, seed=77 + rank, n_distinct=min(B, 2048))
-        tx, tu, ty = (torch.from_numpy(a).to(f"cuda:{local}") for a in (xs, us, ys))
-        warm()
-        ctx.set_state(synthetic_u_old(cfg, B, np.random.default_rng(78 + rank)),
-                      np.zeros((B * S, cfg.nV)), np.zeros(B * S, np.uint32))
-        ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
-        ctx.build()
-        ctx.init_warmstart()
-        ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
-        ctx.step(K, cmpc.CMPC_APPLY_MOVE)
-        ctx.synchronize()
-        reps = max(3, args.steps // 5)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
-        ctx.synchronize()
-        t_prod = (time.perf_counter() - t0) / reps
-        ctx.enable_timing(True)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
-            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
-        ctx.synchronize()
-        t_cl = (time.perf_counter() - t0) / reps
-        kms = lambda k: ctx.kernel_time(k)[0] / max(ctx.kernel_time(k)[1], 1)
-        cl_kernels = {"produce": kms(cmpc.CMPC_KERNEL_PRODUCE), "build": kms(cmpc.CMPC_KERNEL_BUILD),
-                      "iterate": kms(cmpc.CMPC_KERNEL_ITERATE)}
-        ctx.enable_timing(False)
-        _, st_cl, _ = ctx.download()
-        _, _, ws_cl = ctx.get_state()
-        closed = {"ms_per_step": t_cl * 1e3, "producer_ms": t_prod * 1e3,
-                  "kernels_ms": cl_kernels,
-                  "qp_status_ok_fraction": float((st_cl == 0).mean()),
-                  "qp_active_constraint_fraction": float((ws_cl != 0).mean()),
-                  "qp_solves_per_s": B * S * K / t_cl,
-                  "note": "device producer (plant linearisation + discretisation + records) + build "
-                          "+ K iterations with the move applied; synthetic plant states held fixed "
-                          "(no plant simulation), so applied moves accumulate step to step"}
-        # the full receding-horizon step with the per-sub-controller observer
-        # (SURVEY §8(f) row 2): a posteriori update + linearisation at each
-        # slot's x_hat, build, K iterations, a priori update + u_old += du
+    if not args.headline_only:
         try:
-            # the reference runs' gain M = [0; I], identified from their records
-            # (cmpc.reference_observer_gain, tests/test_closed_loop_golden.py)
-            Mg = cmpc.reference_observer_gain(cfg, ys.shape[1])
-            for s_ in range(S):
-                ctx.set_observer(s_, Mg)
+            warm()
+            for i in range(2):
+                ctx.bind_lin(batches[i % NB].data_ptr())
+                ctx.step(1, 0)
+            ctx.synchronize()
+            reps1 = max(10, args.steps // 2)
+            t0 = time.perf_counter()
+            for i in range(reps1):
+                ctx.bind_lin(batches[i % NB].data_ptr())
+                ctx.step(1, 0)
+            ctx.synchronize()
+            t_k1 = (time.perf_counter() - t0) / reps1
+            k1 = {"qp_solves_per_s_per_gpu": B * S / t_k1, "ms_per_step": t_k1 * 1e3, "steps": reps1,
+                  "note": "K = 1 Jacobi iteration per step (build-dominated), this rank's GPU"}
+        except Exception as e:  # reported, never required
+            log(f"K=1 variant failed: {e}")
+
+        # Closed-loop variant (reported beside the metric, not in `value`): the
+        # records are produced on the device from plant states each step
+        # (cmpc_produce_lin), then build + K iterations with
+        # the first move applied.
+    closed = None
+    if not args.headline_only:
+        try:
+            from cmpc.synthetic import synthetic_operating_points, synthetic_u_old
+            xs, us, ys = synthetic_operating_points(cfg, B, seed=77 + rank, n_distinct=min(B, 2048))
+            tx, tu, ty = (torch.from_numpy(a).to(f"cuda:{local}") for a in (xs, us, ys))
             warm()
             ctx.set_state(synthetic_u_old(cfg, B, np.random.default_rng(78 + rank)),
                           np.zeros((B * S, cfg.nV)), np.zeros(B * S, np.uint32))
-            ctx.observer_init(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+            ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
             ctx.build()
             ctx.init_warmstart()
+            ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
             ctx.synchronize()
-            # the isolated kernel timings below advance the observer and the
-            # plans without the build/iterate between them: snapshot the
-            # state and restore it before the full-step loop
-            obs_snap, state_snap = ctx.observer_state(), ctx.get_state()
+            reps = max(3, args.steps // 5)
             t0 = time.perf_counter()
             for _ in range(reps):
-                ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+                ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
             ctx.synchronize()
-            t_os = (time.perf_counter() - t0) / reps
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ctx.observe_apply()
-            ctx.synchronize()
-            t_oa = (time.perf_counter() - t0) / reps
-            ctx.set_observer_state(obs_snap)
-            ctx.set_state(*state_snap)
-            warm()
+            t_prod = (time.perf_counter() - t0) / reps
             ctx.enable_timing(True)
             t0 = time.perf_counter()
             for _ in range(reps):
-                ctx.observe_step(tu.data_ptr(), ty.data_ptr())
-                ctx.build()
-                ctx.iterate(K)
-                ctx.observe_apply()
+                ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+                ctx.step(K, cmpc.CMPC_APPLY_MOVE)
             ctx.synchronize()
-            t_full = (time.perf_counter() - t0) / reps
-            obs_kernels = {"observe_post": kms(cmpc.CMPC_KERNEL_OBSERVE_POST),
-                           "produce_per_qp": kms(cmpc.CMPC_KERNEL_PRODUCE),
-                           "build": kms(cmpc.CMPC_KERNEL_BUILD), "iterate": kms(cmpc.CMPC_KERNEL_ITERATE),
-                           "observe_prior": kms(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
+            t_cl = (time.perf_counter() - t0) / reps
+            kms = lambda k: ctx.kernel_time(k)[0] / max(ctx.kernel_time(k)[1], 1)
+            cl_kernels = {"produce": kms(cmpc.CMPC_KERNEL_PRODUCE), "build": kms(cmpc.CMPC_KERNEL_BUILD),
+                          "iterate": kms(cmpc.CMPC_KERNEL_ITERATE)}
             ctx.enable_timing(False)
-            _, st_o, _ = ctx.download()
-            closed["with_observer"] = {
-                "ms_per_step": t_full * 1e3, "kernels_ms": obs_kernels, "observe_step_ms": t_os * 1e3,
-                "observe_apply_ms": t_oa * 1e3,
-                "qp_status_ok_fraction": float((st_o == 0).mean()),
-                "qp_solves_per_s": B * S * K / t_full,
-                "note": "observe a posteriori + per-QP linearisation at x_hat (records), build, "
-                        "K iterations, observe a priori + u_old update; measured y held fixed, "
-                        f"the reference runs' observer gain [0; I], {reps} consecutive steps"}
-        except Exception as e:
-            log(f"observer closed-loop variant failed: {e}")
-    except Exception as e:  # reported, never required
-        log(f"closed-loop variant failed: {e}")
-    # The whole closed loop of the reference's runs for B scenarios at once
-    # (cmpc/driver.py: plant interval with the input delay line, observer,
-    # build, K iterations, u_old update), this configuration, the reference
-    # runs' observer gain, operating points 0.2 % around the default one
-    if closed is not None:
-        try:
-            from cmpc.driver import ClosedLoop
-            x_def, u_def = cmpc.plant_default(cfg.plant)
-            rng_p = np.random.default_rng(79 + rank)
-            x0s = x_def[None, :] * (1 + 0.002 * rng_p.uniform(-1, 1, (B, len(x_def))))
-            M_ref = cmpc.reference_observer_gain(cfg)
-            loop = ClosedLoop(cfg, arrays, [M_ref] * S, x0s, np.tile(u_def, (B, 1)), K, device=local)
+            _, st_cl, _ = ctx.download()
+            _, _, ws_cl = ctx.get_state()
+            closed = {"ms_per_step": t_cl * 1e3, "producer_ms": t_prod * 1e3,
+                      "kernels_ms": cl_kernels,
+                      "qp_status_ok_fraction": float((st_cl == 0).mean()),
+                      "qp_active_constraint_fraction": float((ws_cl != 0).mean()),
+                      "qp_solves_per_s": B * S * K / t_cl,
+                      "note": "device producer (plant linearisation + discretisation + records) + build "
+                              "+ K iterations with the move applied; synthetic plant states held fixed "
+                              "(no plant simulation), so applied moves accumulate step to step"}
+            # the full receding-horizon step with the per-sub-controller observer
+            # (SURVEY §8(f) row 2): a posteriori update + linearisation at each
+            # slot's x_hat, build, K iterations, a priori update + u_old += du
             try:
-                loop.initialize()
-                for _ in range(3):
-                    loop.step()
+                # the reference runs' gain M = [0; I], identified from their records
+                # (cmpc.reference_observer_gain, tests/test_closed_loop_golden.py)
+                Mg = cmpc.reference_observer_gain(cfg, ys.shape[1])
+                for s_ in range(S):
+                    ctx.set_observer(s_, Mg)
                 warm()
-                torch.cuda.synchronize(local)
-                reps_p = max(5, args.steps // 5)
+                ctx.set_state(synthetic_u_old(cfg, B, np.random.default_rng(78 + rank)),
+                              np.zeros((B * S, cfg.nV)), np.zeros(B * S, np.uint32))
+                ctx.observer_init(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+                ctx.build()
+                ctx.init_warmstart()
+                ctx.synchronize()
+                # the isolated kernel timings below advance the observer and the
+                # plans without the build/iterate between them: snapshot the
+                # state and restore it before the full-step loop
+                obs_snap, state_snap = ctx.observer_state(), ctx.get_state()
                 t0 = time.perf_counter()
-                for _ in range(reps_p):
-                    loop.step()
-                torch.cuda.synchronize(local)
-                t_p = (time.perf_counter() - t0) / reps_p
-                # the same steps again with the library's kernels event-timed
-                loop.ctx.enable_timing(True)
-                for _ in range(reps_p):
-                    loop.step()
-                torch.cuda.synchronize(local)
-                lk = lambda k: loop.ctx.kernel_time(k)[0] / max(loop.ctx.kernel_time(k)[1], 1)
-                plant_kernels = {"observe_post": lk(cmpc.CMPC_KERNEL_OBSERVE_POST),
-                                 "produce_per_qp": lk(cmpc.CMPC_KERNEL_PRODUCE),
-                                 "build": lk(cmpc.CMPC_KERNEL_BUILD), "iterate": lk(cmpc.CMPC_KERNEL_ITERATE),
-                                 "observe_prior": lk(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
-                loop.ctx.enable_timing(False)
-                _, st_p, _ = loop.ctx.download()
-                _, _, _, sst = loop.sim.download()
-            finally:
-                loop.close()
-            closed["with_plant"] = {
-                "ms_per_step": t_p * 1e3, "scenario_steps_per_s": B / t_p, "qp_solves_per_s": B * S * K / t_p,
-                "kernels_ms": plant_kernels,
-                "qp_status_ok_fraction": float((st_p == 0).mean()), "plant_step_failures": int((sst != 0).sum()),
-                "steps": reps_p,
-                "note": "cmpc.driver.ClosedLoop: y = plant output, observe a posteriori + per-QP "
-                        "linearisation, build, K iterations, observe a priori, u_old += own first "
-                        "moves, input delay line, controlled Dormand-Prince over Ts = 0.05 s; "
-                        "observer gain [0; I]; the reference's recorded step (controller only, "
-                        "one scenario, p = 100) is 900.4 us"}
+                for _ in range(reps):
+                    ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+                ctx.synchronize()
+                t_os = (time.perf_counter() - t0) / reps
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    ctx.observe_apply()
+                ctx.synchronize()
+                t_oa = (time.perf_counter() - t0) / reps
+                ctx.set_observer_state(obs_snap)
+                ctx.set_state(*state_snap)
+                warm()
+                ctx.enable_timing(True)
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    ctx.observe_step(tu.data_ptr(), ty.data_ptr())
+                    ctx.build()
+                    ctx.iterate(K)
+                    ctx.observe_apply()
+                ctx.synchronize()
+                t_full = (time.perf_counter() - t0) / reps
+                obs_kernels = {"observe_post": kms(cmpc.CMPC_KERNEL_OBSERVE_POST),
+                               "produce_per_qp": kms(cmpc.CMPC_KERNEL_PRODUCE),
+                               "build": kms(cmpc.CMPC_KERNEL_BUILD), "iterate": kms(cmpc.CMPC_KERNEL_ITERATE),
+                               "observe_prior": kms(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
+                ctx.enable_timing(False)
+                _, st_o, _ = ctx.download()
+                closed["with_observer"] = {
+                    "ms_per_step": t_full * 1e3, "kernels_ms": obs_kernels, "observe_step_ms": t_os * 1e3,
+                    "observe_apply_ms": t_oa * 1e3,
+                    "qp_status_ok_fraction": float((st_o == 0).mean()),
+                    "qp_solves_per_s": B * S * K / t_full,
+                    "note": "observe a posteriori + per-QP linearisation at x_hat (records), build, "
+                            "K iterations, observe a priori + u_old update; measured y held fixed, "
+                            f"the reference runs' observer gain [0; I], {reps} consecutive steps"}
+            except Exception as e:
+                log(f"observer closed-loop variant failed: {e}")
         except Exception as e:  # reported, never required
-            log(f"closed loop with the plant failed: {e}")
-    # SURVEY config 4 (sub-controllers sharded over the ranks, RCCL all-gather
-    # of the plans once per Jacobi iteration), beside the metric: every rank
-    # takes part, so at world N it times the exchange over xGMI
+            log(f"closed-loop variant failed: {e}")
+        # The whole closed loop of the reference's runs for B scenarios at once
+        # (cmpc/driver.py: plant interval with the input delay line, observer,
+        # build, K iterations, u_old update), this configuration, the reference
+        # runs' observer gain, operating points 0.2 % around the default one
+        if closed is not None:
+            try:
+                from cmpc.driver import ClosedLoop
+                x_def, u_def = cmpc.plant_default(cfg.plant)
+                rng_p = np.random.default_rng(79 + rank)
+                x0s = x_def[None, :] * (1 + 0.002 * rng_p.uniform(-1, 1, (B, len(x_def))))
+                M_ref = cmpc.reference_observer_gain(cfg)
+                loop = ClosedLoop(cfg, arrays, [M_ref] * S, x0s, np.tile(u_def, (B, 1)), K, device=local)
+                try:
+                    loop.initialize()
+                    for _ in range(3):
+                        loop.step()
+                    warm()
+                    torch.cuda.synchronize(local)
+                    reps_p = max(5, args.steps // 5)
+                    t0 = time.perf_counter()
+                    for _ in range(reps_p):
+                        loop.step()
+                    torch.cuda.synchronize(local)
+                    t_p = (time.perf_counter() - t0) / reps_p
+                    # the same steps again with the library's kernels event-timed
+                    loop.ctx.enable_timing(True)
+                    for _ in range(reps_p):
+                        loop.step()
+                    torch.cuda.synchronize(local)
+                    lk = lambda k: loop.ctx.kernel_time(k)[0] / max(loop.ctx.kernel_time(k)[1], 1)
+                    plant_kernels = {"observe_post": lk(cmpc.CMPC_KERNEL_OBSERVE_POST),
+                                     "produce_per_qp": lk(cmpc.CMPC_KERNEL_PRODUCE),
+                                     "build": lk(cmpc.CMPC_KERNEL_BUILD), "iterate": lk(cmpc.CMPC_KERNEL_ITERATE),
+                                     "observe_prior": lk(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
+                    loop.ctx.enable_timing(False)
+                    _, st_p, _ = loop.ctx.download()
+                    n_fail, _ = loop.plant_failures()   # sticky: every interval since initialize
+                finally:
+                    loop.close()
+                closed["with_plant"] = {
+                    "ms_per_step": t_p * 1e3, "scenario_steps_per_s": B / t_p, "qp_solves_per_s": B * S * K / t_p,
+                    "kernels_ms": plant_kernels,
+                    "qp_status_ok_fraction": float((st_p == 0).mean()), "plant_step_failures": n_fail,
+                    "steps": reps_p,
+                    "note": "cmpc.driver.ClosedLoop: y = plant output, observe a posteriori + per-QP "
+                            "linearisation, build, K iterations, observe a priori, u_old += own first "
+                            "moves, input delay line, controlled Dormand-Prince over Ts = 0.05 s; "
+                            "observer gain [0; I]; the reference's recorded step (controller only, "
+                            "one scenario, p = 100) is 900.4 us"}
+            except Exception as e:  # reported, never required
+                log(f"closed loop with the plant failed: {e}")
+        # SURVEY config 4 (sub-controllers sharded over the ranks, RCCL all-gather
+        # of the plans once per Jacobi iteration), beside the metric: every rank
+        # takes part, so at world N it times the exchange over xGMI
     coupled = None
-    if not args.no_coupled:
+    if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench
         rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
                                steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds)
@@ -627,7 +632,7 @@ def main():
         "closed_loop_device_resident": closed,
         "coupled": coupled,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not args.headline_only:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, arrays, lin0, u_old, K, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never required

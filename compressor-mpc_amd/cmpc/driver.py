@@ -166,6 +166,15 @@ class ClosedLoop:
         self.k += 1
         return t, y
 
+    def plant_failures(self):
+        """Scenarios whose plant integration failed in any interval since
+        initialize (the simulator's status is sticky: 1 step-size control, 2
+        more than 500 steps in an interval, 3 non-finite), as (count, status
+        per scenario).  The reference's odeint throws and ends the run; here a
+        failed scenario stops where it failed and the rest carry on."""
+        st = self.sim.download()[3]
+        return int((st != 0).sum()), st
+
     @staticmethod
     def torch_ptr(t):
         import ctypes

@@ -251,26 +251,44 @@ hipError_t pooled_event(cmpc_ctx* c, hipEvent_t* e) {
 
 // A timed launch: the launcher (cmpc_launch, cmpc_internal.h) passes both
 // events to hipExtLaunchKernelGGL, which writes the kernel's start and end
-// into them; no marker packets go into the stream.
-int timed_begin(cmpc_ctx* c, int k, hipEvent_t* e0) {
-  cmpc_launch_events = LaunchEvents{};
-  if (!((c->timing >> k) & 1)) return 0;
-  hipEvent_t e1;
-  HIP_TRY(pooled_event(c, e0));
-  HIP_TRY(pooled_event(c, &e1));
-  cmpc_launch_events.start = *e0;
-  cmpc_launch_events.stop = e1;
-  return 0;
-}
+// into them; no marker packets go into the stream.  The guard hands the events
+// to the context's pending list on end() and, on any early return (a failed
+// launch), clears cmpc_launch_events and gives them back to the pool.
+class TimedLaunch {
+ public:
+  TimedLaunch(cmpc_ctx* c, int k) : c_(c), k_(k) {}
+  TimedLaunch(const TimedLaunch&) = delete;
+  TimedLaunch& operator=(const TimedLaunch&) = delete;
+  int begin() {
+    cmpc_launch_events = LaunchEvents{};
+    if (!((c_->timing >> k_) & 1)) return 0;
+    HIP_TRY(pooled_event(c_, &e0_));
+    HIP_TRY(pooled_event(c_, &e1_));
+    cmpc_launch_events.start = e0_;
+    cmpc_launch_events.stop = e1_;
+    return 0;
+  }
+  int end() {
+    cmpc_launch_events = LaunchEvents{};
+    if (e0_ && e1_) {
+      c_->pending[k_].push_back({e0_, e1_});
+      c_->launches[k_]++;
+    }
+    e0_ = e1_ = nullptr;
+    return 0;
+  }
+  ~TimedLaunch() {
+    if (!e0_ && !e1_) return;
+    cmpc_launch_events = LaunchEvents{};
+    if (e0_) c_->event_pool.push_back(e0_);
+    if (e1_) c_->event_pool.push_back(e1_);
+  }
 
-int timed_end(cmpc_ctx* c, int k, hipEvent_t e0) {
-  const hipEvent_t e1 = cmpc_launch_events.stop;
-  cmpc_launch_events = LaunchEvents{};
-  if (!((c->timing >> k) & 1)) return 0;
-  c->pending[k].push_back({e0, e1});
-  c->launches[k]++;
-  return 0;
-}
+ private:
+  cmpc_ctx* c_;
+  int k_;
+  hipEvent_t e0_ = nullptr, e1_ = nullptr;
+};
 
 int resolve_timing(cmpc_ctx* c) {
   for (int k = 0; k < CMPC_KERNEL_COUNT; ++k) {
@@ -606,11 +624,11 @@ int cmpc_produce_lin(cmpc_ctx* c, int plant, double p_in, double p_out, double T
   P.y = y;
   HIP_TRY(hipSetDevice(c->device));
   c->lin_bound = nullptr;  // the build reads the produced records
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_PRODUCE, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_PRODUCE);
+  if (tl.begin()) return -1;
   if (cmpc_launch_produce(P, plant, c->stream)) return fail("cmpc_produce_lin: launch failed");
   if (check_launch("produce kernel")) return -1;
-  return timed_end(c, CMPC_KERNEL_PRODUCE, e0);
+  return tl.end();
 }
 
 // ---- observer ----
@@ -670,8 +688,9 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
   if (c->obs_nout && c->obs_nout != n_outputs)
     return fail("cmpc_set_observer: n_outputs differs between sub-controllers");
   if (c->L.nobs > 32) return fail("cmpc_set_observer: ns + ndist > 32");
-  if (cmpc_obs_prior_shape(c->L.ntot - c->L.nobs, c->L.nd, d.nu_tot) <= 0)
-    return fail("cmpc_set_observer: more than 16 inputs or delayed inputs per sub-controller");
+  if (!cmpc_obs_supported(d.ns, n_outputs, d.ndist, c->L.ntot - c->L.nobs, c->L.nd, d.nu_tot))
+    return fail("cmpc_set_observer: no observer kernel for these dimensions (instantiated: ns 10 or 11, "
+                "4 outputs, 4 disturbance states, 4 inputs)");
   for (int i = 0; i < d.nu_tot; ++i)
     if (d.delay[i] == 1) return fail("cmpc_set_observer: a one-step input delay has no delay block");
   HIP_TRY(hipSetDevice(c->device));
@@ -726,11 +745,11 @@ static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) 
   P.u_full = u_full;
   P.y = y;
   c->lin_bound = nullptr;
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_PRODUCE, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_PRODUCE);
+  if (tl.begin()) return -1;
   if (cmpc_launch_produce(P, c->obs_plant, c->stream)) return fail("observer: produce launch failed");
   if (check_launch("produce kernel (per QP)")) return -1;
-  return timed_end(c, CMPC_KERNEL_PRODUCE, e0);
+  return tl.end();
 }
 
 int cmpc_observer_init(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
@@ -775,11 +794,11 @@ int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
   ObserverParams P;
   observer_params(c, &P);
   P.y = y;
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_OBSERVE_POST, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_OBSERVE_POST);
+  if (tl.begin()) return -1;
   if (cmpc_launch_observer(P, CMPC_OBS_POST, c->stream)) return fail("observer launch failed");
   if (check_launch("observer a-posteriori kernel")) return -1;
-  if (timed_end(c, CMPC_KERNEL_OBSERVE_POST, e0)) return -1;
+  if (tl.end()) return -1;
   return observer_produce(c, u_full, y);
 }
 
@@ -790,13 +809,13 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   ObserverParams P;
   observer_params(c, &P);
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_OBSERVE_PRIOR, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_OBSERVE_PRIOR);
+  if (tl.begin()) return -1;
   if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream))
     return fail("cmpc_observe_apply: no a-priori kernel instantiation for these dimensions");
   if (check_launch("observer a-priori kernel")) return -1;
   c->obs_steps++;  // the delay-block rings advance by one
-  return timed_end(c, CMPC_KERNEL_OBSERVE_PRIOR, e0);
+  return tl.end();
 }
 
 // copies host arrays (nullptr entries skipped) into the context's staging
@@ -906,7 +925,9 @@ int cmpc_sim_create(cmpc_sim** out, int plant, int B, int device, double p_in, d
       (e = hipMalloc(&m->scratch, sizeof(double) * Bz * (ni > n_control ? ni : n_control))) != hipSuccess ||
       (e = hipMalloc(&m->stage, sizeof(double) * Bz * 2 * std::max(std::max(ns, ni), std::max(no, n_control)))) !=
           hipSuccess ||
-      (e = hipMalloc(&m->status, sizeof(int32_t) * Bz)) != hipSuccess)
+      (e = hipMalloc(&m->status, sizeof(int32_t) * Bz)) != hipSuccess ||
+      (e = hipMemsetAsync(m->status, 0, sizeof(int32_t) * Bz, m->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(m->stream)) != hipSuccess)
     return bail(e);
   *out = m;
   return 0;
@@ -968,6 +989,7 @@ int cmpc_sim_reset(cmpc_sim* m, const double* x0, const double* u_offset, double
   HIP_TRY(hipMemcpyAsync(m->dt, dts.data(), sizeof(double) * Bz, hipMemcpyHostToDevice, m->stream));
   // TimeDelay(): zero memory, cursor of input i at the sum of the delays before it
   HIP_TRY(hipMemsetAsync(m->ring, 0, sizeof(double) * Bz * m->ring_len, m->stream));
+  HIP_TRY(hipMemsetAsync(m->status, 0, sizeof(int32_t) * Bz, m->stream));  // failures are sticky until here
   for (int i = 0, sum = 0; i < m->nc; ++i) {
     m->cur[i] = sum;
     sum += m->delay[i];
@@ -1358,8 +1380,8 @@ int cmpc_build(cmpc_ctx* c) {
     P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
   }
   cmpc_rows_layout(d, L.nd, L.nobs, L.rec_len, &P.rows);  // cached per dimension set
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_BUILD, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_BUILD);
+  if (tl.begin()) return -1;
   int rc = -1;
   // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
   // than the one-QP-per-wave kernel for every plant/controller type at
@@ -1379,7 +1401,7 @@ int cmpc_build(cmpc_ctx* c) {
     c->last_build = CMPC_BUILD_WAVE;
   }
   if (check_launch("build kernel")) return -1;
-  return timed_end(c, CMPC_KERNEL_BUILD, e0);
+  return tl.end();
 }
 
 int cmpc_init_warmstart(cmpc_ctx* c) {
@@ -1419,12 +1441,12 @@ int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
     P.ntrace = c->ntrace;
     c->trace_K = K;
   }
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_ITERATE, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_ITERATE);
+  if (tl.begin()) return -1;
   if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
     return fail("solve kernel not instantiated for these dimensions");
   if (check_launch("iterate kernel")) return -1;
-  return timed_end(c, CMPC_KERNEL_ITERATE, e0);
+  return tl.end();
 }
 
 int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, const double* G_ext,
@@ -1460,12 +1482,12 @@ int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, co
   P.s_offset = s_offset;
   P.B = c->nqp / S_local;
   P.flags = flags;
-  hipEvent_t e0 = nullptr;
-  if (timed_begin(c, CMPC_KERNEL_ITERATE, &e0)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_ITERATE);
+  if (tl.begin()) return -1;
   if (cmpc_launch_coupled(P, c->L.nV, c->d.nu, c->stream))
     return fail("coupled kernel not instantiated for these dimensions (nV = 4, nu = 2)");
   if (check_launch("coupled kernel")) return -1;
-  return timed_end(c, CMPC_KERNEL_ITERATE, e0);
+  return tl.end();
 }
 
 int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {

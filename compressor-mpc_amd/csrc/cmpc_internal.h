@@ -230,5 +230,6 @@ int cmpc_launch_sim_output(int plant, const double* x, double* y, int B, void* s
 
 int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream);
 int cmpc_obs_prior_shape(int n_aug, int nd, int nu_tot);
+bool cmpc_obs_supported(int ns, int n_out, int ndist, int n_aug, int nd, int nu_tot);
 int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream);
 int cmpc_launch_coupled(const CoupledParams& P, int n, int nu, void* stream);

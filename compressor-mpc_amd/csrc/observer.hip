@@ -200,6 +200,15 @@ int cmpc_obs_prior_shape(int n_aug, int nd, int nu_tot) {
   return (nd <= 16 && nu_tot <= 16) ? 4 : 0;
 }
 
+// The observer kernels instantiated below: both compressor plants (ns 11 /
+// 10), four outputs and four disturbance states, four inputs.  cmpc_set_observer
+// checks the same predicate, so an unsupported shape fails at set-up rather
+// than at the first cmpc_observe_step / cmpc_observe_apply.
+bool cmpc_obs_supported(int ns, int n_out, int ndist, int n_aug, int nd, int nu_tot) {
+  return (ns == 11 || ns == 10) && n_out == 4 && ndist == 4 && nu_tot == 4 &&
+         cmpc_obs_prior_shape(n_aug, nd, nu_tot) > 0;
+}
+
 int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (P.nqp <= 0) return 0;
@@ -209,6 +218,7 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       hipLaunchKernelGGL(cmpc_obs_init_kernel, dim3(grid), dim3(64 * kWaves), 0, s, P);
       return 0;
     case CMPC_OBS_POST: {
+      if (!cmpc_obs_supported(P.ns, P.n_out, P.ndist, P.ntot - P.nobs, P.nd, P.nu_tot)) return -1;
       const int g4 = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
       if (P.ns == 11 && P.n_out == 4 && P.ndist == 4)
         cmpc_launch((cmpc_obs_post_kernel<11, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
@@ -219,7 +229,7 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
       return 0;
     }
     case CMPC_OBS_PRIOR: {
-      if (cmpc_obs_prior_shape(P.ntot - P.nobs, P.nd, P.nu_tot) <= 0 || P.nu_tot != 4) return -1;
+      if (!cmpc_obs_supported(P.ns, P.n_out, P.ndist, P.ntot - P.nobs, P.nd, P.nu_tot)) return -1;
       const int g = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
       if (P.ns == 11)
         cmpc_launch((cmpc_obs_prior_kernel<11, 4>), dim3(g), dim3(64 * kWaves), 0, s, P);

@@ -55,6 +55,10 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
   constexpr int N = F::ns, NI = F::ni;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= P.B) return;
+  // the status is sticky: a scenario that failed in an earlier interval
+  // stays where it stopped (the reference's odeint throws and the run ends)
+  // until cmpc_sim_reset clears it
+  if (P.status[b]) return;
   double x[N], k1[N], u[NI];
 #pragma unroll
   for (int i = 0; i < N; ++i) x[i] = P.x[(size_t)b * N + i];
@@ -108,6 +112,10 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
         acc += r * r;
       }
       double err = sqrt(acc);
+      if (!(err == err) || err > 1.7976931348623157e308) {  // non-finite error norm
+        status = 3;
+        break;
+      }
       if (err > 1.0) {  // reject: dt *= max(0.9 err^(-1/3), 0.2)
         const double f = 0.9 * pow(err, -1.0 / 3.0);
         dt *= f > 0.2 ? f : 0.2;
@@ -123,11 +131,14 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
         if (err < lo) err = lo;
         dt *= 0.9 * pow(err, -1.0 / 5.0);
       }
+      bool finite = true;
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         x[i] = xo[i];
         k1[i] = k7[i];  // FSAL
+        finite = finite && fabs(xo[i]) <= 1.7976931348623157e308;
       }
+      if (!finite) status = 3;
       break;
     }
     if (status) break;
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(64) void cmpc_sim_kernel(SimParams P) {
 #pragma unroll
   for (int i = 0; i < N; ++i) P.x[(size_t)b * N + i] = x[i];
   P.dt[b] = dt;
-  if (P.status) P.status[b] = status;
+  if (status) P.status[b] = status;
 }
 
 // SetInput: TimeDelay::GetDelayedInput then GetPlantInput (u_offset + delayed

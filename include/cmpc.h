@@ -256,7 +256,13 @@ int cmpc_coupled_iterate(cmpc_ctx* ctx, int S_total, int S_local, int s_offset,
  *                                  ObserveAPriori (observer.cc:8-22) with the own
  *                                  first move (other inputs zero,
  *                                  nerve_center.h:323-328), then u_old += du
- * All device pointers; asynchronous on the context's stream. */
+ * All device pointers; asynchronous on the context's stream.
+ * Not graph-capturable: the delay blocks' ring phase (a-priori steps since
+ * cmpc_observer_init) is host state that reaches the kernels as a launch
+ * argument and advances per cmpc_observe_apply call, so a replayed capture
+ * would reuse the phase it was captured with.  The same holds for
+ * cmpc_sim_set_input (the TimeDelay cursors).  cmpc_build, cmpc_iterate and
+ * cmpc_step carry no such host state. */
 /* ObserverMatrix M of sub-controller s ((ns + ndist) x n_outputs, row-major;
  * the DistributedController constructor argument, distributed_controller.cc:14).
  * n_outputs (the plant's outputs, ObserverOutputIndices) must agree for all s. */
@@ -319,7 +325,11 @@ int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);
  * Device arrays: cmpc_sim_state (x), cmpc_sim_input (plant input u_),
  * cmpc_sim_step_size (dt), cmpc_sim_status (1 = step-size control failed:
  * 500 rejected tries of one step; 2 = more than 500 steps in one interval,
- * odeint's max_step_checker; the scenario's state stays where it stopped). */
+ * odeint's max_step_checker; 3 = non-finite error norm or state). A status
+ * is sticky: the scenario's state stays where it stopped and later
+ * cmpc_sim_integrate calls skip it (the reference's odeint throws and ends
+ * the run) until cmpc_sim_reset clears it, so one read after a run counts
+ * every scenario that failed in any interval. */
 typedef struct cmpc_sim cmpc_sim;
 int cmpc_sim_create(cmpc_sim** sim, int plant, int B, int device, double p_in, double p_out,
                     int n_control, const int32_t* delays /* n_control, control order */,

@@ -14,8 +14,11 @@
 //       between observations and started afresh at dt by every call)
 //
 // The plant is selected at run time (cmpc::PlantType) instead of the
-// reference's template argument; Delays / InputIndices are the reference
-// plants' (0, 40, 0, 40) / (0, 3, 4, 7).
+// reference's template argument (simulation_system.h:17); the System object's
+// inlet/outlet pressures and the Delays / InputIndices template arguments
+// (:17, :50) are constructor arguments whose defaults are the reference
+// plants' (p_in = p_out = 1, delays (0, 40, 0, 40), control inputs at plant
+// inputs (0, 3, 4, 7)).
 #pragma once
 
 #include <functional>
@@ -31,14 +34,19 @@ class SimulationSystem {
   using IntegrationCallback = std::function<void(const std::vector<double>& x, double t)>;
 
   SimulationSystem(PlantType plant, const std::vector<double>& u_offset, const std::vector<double>& x_in,
-                   int device = 0, double dt0 = 0.05)
+                   int device = 0, double dt0 = 0.05, double p_in = 1.0, double p_out = 1.0,
+                   const std::vector<int32_t>& delays = {0, 40, 0, 40},
+                   const std::vector<int32_t>& input_indices = {0, 3, 4, 7})
       : plant_(plant) {
     int nci = 0;
     Check(cmpc_plant_dims(static_cast<int>(plant), &ns_, &ni_, &no_, &nci), "cmpc_plant_dims");
     if (static_cast<int>(u_offset.size()) != ni_ || static_cast<int>(x_in.size()) != ns_)
       throw Error("SimulationSystem: u_offset needs n_inputs, x_in n_states values");
-    const int32_t delays[4] = {0, 40, 0, 40}, cidx[4] = {0, 3, 4, 7};
-    Check(cmpc_sim_create(&sim_, static_cast<int>(plant), 1, device, 1.0, 1.0, 4, delays, cidx),
+    if (delays.size() != input_indices.size() || delays.empty())
+      throw Error("SimulationSystem: one delay per control input");
+    nc_ = static_cast<int>(delays.size());
+    Check(cmpc_sim_create(&sim_, static_cast<int>(plant), 1, device, p_in, p_out, nc_, delays.data(),
+                          input_indices.data()),
           "cmpc_sim_create");
     Check(cmpc_sim_reset_host(sim_, x_in.data(), u_offset.data(), dt0), "cmpc_sim_reset_host");
   }
@@ -63,7 +71,7 @@ class SimulationSystem {
     Check(cmpc_sim_set_offset_host(sim_, u_offset.data()), "cmpc_sim_set_offset_host");
   }
   void SetInput(const std::vector<double>& u_control) {
-    if (u_control.size() != 4) throw Error("SetInput: 4 control inputs");
+    if (static_cast<int>(u_control.size()) != nc_) throw Error("SetInput: one value per control input");
     Check(cmpc_sim_set_input_host(sim_, u_control.data()), "cmpc_sim_set_input_host");
   }
   std::vector<double> GetOutput() const {
@@ -88,8 +96,9 @@ class SimulationSystem {
       Check(cmpc_sim_integrate(sim_, t, t + dt, max_abs_error, max_rel_error), "cmpc_sim_integrate");
       int32_t st = 0;
       Check(cmpc_sim_download(sim_, nullptr, nullptr, nullptr, &st), "cmpc_sim_download");
-      if (st) throw Error(st == 2 ? "Integrate: more than 500 steps in one observation interval"
-                                  : "Integrate: step size control failed");
+      if (st) throw Error(st == 2   ? "Integrate: more than 500 steps in one observation interval"
+                          : st == 3 ? "Integrate: non-finite state or error norm"
+                                    : "Integrate: step size control failed");
       ++step;
       t = t0 + static_cast<double>(step) * dt;
     }
@@ -102,7 +111,7 @@ class SimulationSystem {
 
  private:
   PlantType plant_;
-  int ns_ = 0, ni_ = 0, no_ = 0;
+  int ns_ = 0, ni_ = 0, no_ = 0, nc_ = 0;
   cmpc_sim* sim_ = nullptr;
 };
 

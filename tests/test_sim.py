@@ -183,6 +183,28 @@ def test_gpu_sim_step_bound():
             x, _, _, st = sim.download()
             assert st[0] == 0 and st[1] == (2 if k == 10 else 0), (k, st)
         np.testing.assert_allclose(x[0], good.x, rtol=1e-12)
+        # sticky: a later interval — clean or not — neither clears
+        # status 2 nor moves the failed scenario on from where it stopped
+        x_stop = x[1].copy()
+        for k in range(11, 14):
+            sim.set_input(dev(np.zeros((2, 4))))
+            sim.integrate(k * TS, k * TS + TS)
+            good.set_input(np.zeros(4))
+            good.integrate(k * TS, k * TS + TS)
+        x, _, _, st = sim.download()
+        assert st[0] == 0 and st[1] == 2, st
+        np.testing.assert_array_equal(x[1], x_stop)
+        np.testing.assert_allclose(x[0], good.x, rtol=1e-12)
+        # a non-finite state fails with status 3 instead of passing as 0
+        xn = np.stack([x0, x0])
+        xn[1, 2] = np.nan
+        sim.reset(dev(xn), dev(np.stack([u0, u0])), TS)
+        x, _, _, st = sim.download()
+        assert not st.any(), st                    # reset clears the sticky status
+        sim.set_input(dev(np.zeros((2, 4))))
+        sim.integrate(0.0, TS)
+        x, _, _, st = sim.download()
+        assert st[0] == 0 and st[1] == 3, st
 
 
 # ---- the closed-loop driver (cmpc/driver.py) -----------------------------------

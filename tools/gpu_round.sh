@@ -10,12 +10,12 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --headline-only > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
 pmc() {  # name, counters...   (separate passes, kernel trace only)
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace -T --kernel-include-regex 'cmpc_' \
      --pmc "$@" -d gpurun_out/pmc${TAG}_$name -o run --output-format csv -- \
-     python3 bench.py --steps 3 --warmup 1 --no-cpu --settle-seconds 0 > gpurun_out/pmc${TAG}_$name.json 2> gpurun_out/pmc${TAG}_$name.err
+     python3 bench.py --steps 3 --warmup 1 --no-cpu --headline-only --settle-seconds 0 > gpurun_out/pmc${TAG}_$name.json 2> gpurun_out/pmc${TAG}_$name.err
 }
 pmc sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU || exit $?
 pmc sq2 SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 || exit $?
