@@ -90,6 +90,7 @@ EXPORTS = (
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
+    "cmpc_get_input", "cmpc_get_input_host", "cmpc_update_u", "cmpc_update_u_host",
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
     "cmpc_observer_init_host", "cmpc_observe_step_host",
@@ -189,6 +190,10 @@ def load_library(path: str = LIB_PATH):
         "cmpc_accumulate_moves": ([c_void, P(i32), c_void], ctypes.c_int),
         "cmpc_get_observer_state": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_set_observer_state": ([c_void, P(dbl)], ctypes.c_int),
+        "cmpc_get_input": ([c_void, c_void, u32], ctypes.c_int),
+        "cmpc_get_input_host": ([c_void, P(dbl), u32], ctypes.c_int),
+        "cmpc_update_u": ([c_void, c_void], ctypes.c_int),
+        "cmpc_update_u_host": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,
                                   c_void, u32], ctypes.c_int),
         "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),

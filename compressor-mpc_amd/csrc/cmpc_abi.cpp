@@ -1449,6 +1449,68 @@ int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
   return tl.end();
 }
 
+// DistributedController::GetInput (include/distributed_controller.h:206-226):
+// one warm-started solve per slot with the other controllers' plans given.
+int cmpc_get_input(cmpc_ctx* c, const double* du_last, uint32_t flags) {
+  if (!c) return fail("null context");
+  if (flags & CMPC_TRACE) return fail("cmpc_get_input: no trace");
+  if (ensure_cfg(c)) return -1;
+  if (c->L.nVo > 0 && !du_last) return fail("cmpc_get_input: du_last is needed (nu < nu_tot)");
+  if (c->L.nVo == 0) return cmpc_iterate(c, 1, flags);  // full controller: SolveQP(qp_, u_old_)
+  HIP_TRY(hipSetDevice(c->device));
+  SolveParams P;
+  solve_params(c, &P);
+  P.K = 1;
+  P.flags = flags;
+  P.du_other = du_last;
+  TimedLaunch tl(c, CMPC_KERNEL_ITERATE);
+  if (tl.begin()) return -1;
+  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
+    return fail("cmpc_get_input: solve kernel not instantiated for these dimensions");
+  if (check_launch("get-input kernel")) return -1;
+  return tl.end();
+}
+
+int cmpc_get_input_host(cmpc_ctx* c, const double* du_last, uint32_t flags) {
+  if (!c) return fail("null context");
+  if (c->L.nVo == 0 || !du_last) return cmpc_get_input(c, nullptr, flags);
+  HIP_TRY(hipSetDevice(c->device));
+  const double* h[1] = {du_last};
+  const size_t n[1] = {(size_t)c->nqp * c->L.nVo};
+  const double* d[1];
+  if (stage_host(c, h, n, 1, d)) return -1;
+  return cmpc_get_input(c, d[0], flags);
+}
+
+// DistributedController::UpdateU(du) (include/distributed_controller.h:145-152)
+// with the caller's full input change: ObserveAPriori(du, u_old_), u_old_ += du.
+int cmpc_update_u(cmpc_ctx* c, const double* du_full) {
+  if (!c || !du_full) return fail("null argument");
+  if (c->obs_plant < 0) return fail("cmpc_update_u: call cmpc_observer_init first");
+  if (c->lin_bound) return fail("cmpc_update_u: records are bound externally");
+  HIP_TRY(hipSetDevice(c->device));
+  ObserverParams P;
+  observer_params(c, &P);
+  P.du_full = du_full;
+  TimedLaunch tl(c, CMPC_KERNEL_OBSERVE_PRIOR);
+  if (tl.begin()) return -1;
+  if (cmpc_launch_observer(P, CMPC_OBS_PRIOR, c->stream))
+    return fail("cmpc_update_u: no a-priori kernel instantiation for these dimensions");
+  if (check_launch("observer a-priori kernel")) return -1;
+  c->obs_steps++;  // the delay-block rings advance by one
+  return tl.end();
+}
+
+int cmpc_update_u_host(cmpc_ctx* c, const double* du_full) {
+  if (!c || !du_full) return fail("null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const double* h[1] = {du_full};
+  const size_t n[1] = {(size_t)c->nqp * c->d.nu_tot};
+  const double* d[1];
+  if (stage_host(c, h, n, 1, d)) return -1;
+  return cmpc_update_u(c, d[0]);
+}
+
 int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, const double* G_ext,
                          const double* du_all, double* du_out, uint32_t flags) {
   if (!c) return fail("null context");

@@ -102,6 +102,8 @@ struct SolveParams {
   CfgOffsets co;
   uint32_t flags;
   int init;           // 1: InitializeQPProblem (cold, f only, ws only)
+  const double* du_other;  // nqp * nVo other controllers' plans (cmpc_get_input), or null:
+                           // the in-scenario exchange of cmpc_iterate
 };
 
 // Standalone batched solver (parity / KKT tests).
@@ -153,6 +155,8 @@ struct ObserverParams {
   const double* lin;        // step records (prior: B, f)
   const double* du_old;     // nqp * nV plans (prior)
   double* u_old;            // nqp * nu_tot (prior)
+  const double* du_full;    // nqp * nu_tot applied input change (cmpc_update_u), or null:
+                            // the own first move of du_old (cmpc_observe_apply)
   int nqp, S, ns, ndist, nobs, ntot, n_out, obs_len;
   int nu, nu_tot, nV, nd, rec_len, off_B, off_f;
   int delay[CMPC_MAX_INPUTS];   // per input (sub-controller order)

@@ -485,7 +485,10 @@ struct HinvLds {
 // ---------------------------------------------------------------------------
 // Jacobi iterate kernel (lane per QP)
 // ---------------------------------------------------------------------------
-template <int N, int NU, int NVO, bool TRACE>
+// EXT: the other controllers' plans come from P.du_other (one GetInput call of
+// a stand-alone sub-controller, cmpc_get_input) instead of the lanes of the
+// scenario's other slots.
+template <int N, int NU, int NVO, bool TRACE, bool EXT = false>
 __global__ __launch_bounds__(CMPC_SOLVE_THREADS)
 __attribute__((amdgpu_waves_per_eu(CMPC_SOLVE_WPE(N), CMPC_SOLVE_WPE(N))))
 void cmpc_solve_kernel(SolveParams P) {
@@ -578,14 +581,26 @@ void cmpc_solve_kernel(SolveParams P) {
     for (int a = 0; a < N; ++a) fk[a] = f[a];
     if (NVO > 0 && CMPC_QP_ABL != 3) {
       double dother[NVOA];
+      if constexpr (EXT) {
+        // du_last of DistributedController::GetInput: the other controllers'
+        // plans, controller-major, then move, then input (nerve_center.h:283-285)
 #pragma unroll
-      for (int rk = 0; rk < SM1; ++rk) {
-        const int s2 = rk + (rk >= s ? 1 : 0);
+        for (int rk = 0; rk < SM1; ++rk)
 #pragma unroll
-        for (int mv = 0; mv < M; ++mv)
+          for (int mv = 0; mv < M; ++mv)
 #pragma unroll
-          for (int c = 0; c < NU; ++c)
-            dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + s2, 64);
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = P.du_other[(size_t)q * NVO + rk * N + mv * NU + c];
+      } else {
+#pragma unroll
+        for (int rk = 0; rk < SM1; ++rk) {
+          const int s2 = rk + (rk >= s ? 1 : 0);
+#pragma unroll
+          for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + s2, 64);
+        }
       }
       // f_k = f + (Su_other du_other)' W Su  ==  f + G du_other
 #pragma unroll
@@ -703,6 +718,12 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m, void*
   if (nV == N_ && nu == NU_ && nVo == NVO_) {                                          \
     if (P.qp_len != N_ * N_ + N_ + N_ * NVO_) return -1;                               \
     const int grid = (P.nqp + CMPC_SOLVE_THREADS - 1) / CMPC_SOLVE_THREADS;            \
+    if (P.du_other) {                                                                  \
+      if (NVO_ == 0 || P.trace) return -1;                                             \
+      cmpc_launch((cmpc_solve_kernel<N_, NU_, NVO_, false, (NVO_ > 0)>), dim3(grid),   \
+                  dim3(CMPC_SOLVE_THREADS), 0, s, P);                                  \
+      return 0;                                                                        \
+    }                                                                                  \
     if (P.trace)                                                                       \
       cmpc_launch((cmpc_solve_kernel<N_, NU_, NVO_, true>), dim3(grid),                \
                   dim3(CMPC_SOLVE_THREADS), 0, s, P);                                  \

@@ -136,10 +136,12 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
   double* dx = st + NS;
   const double* rec = P.lin + (size_t)q * P.rec_len;
   double* uo = P.u_old + (size_t)q * NUT;
-  // lanes < nu_tot: u_old, du = own first move (others zero, nerve_center.h:323-328)
+  // lanes < nu_tot: u_old, du = own first move (others zero, nerve_center.h:323-328),
+  // or the caller's full input change (DistributedController::UpdateU(du))
   const int li = lane < NUT ? lane : 0;
   const double u0 = uo[li];
-  const double du = (lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0;
+  const double du = P.du_full ? ((lane < NUT) ? P.du_full[(size_t)q * NUT + lane] : 0.0)
+                              : ((lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0);
   // lanes < nd: delayed-input slot, the block's first state (ring head), the
   // input's u_old
   const int lk = lane < nd ? lane : 0;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverPar
     dx[nobs + lane] = first;  // slot k <- first state of block k
     dx[head] = last;          // the ring advances: this entry becomes the last state
   }
-  // UpdateU: u_old += du (own inputs; the others add zero)
+  // UpdateU: u_old += du (cmpc_observe_apply: own inputs, the others add zero)
   if (lane < NUT) uo[lane] = u0 + du;
 }
 

@@ -220,6 +220,29 @@ int cmpc_plant_lin_record(int plant, double p_in, double p_out, double Ts,
                           const int32_t* input_order, const int32_t* out_idx,
                           const cmpc_dims* dims, double* record);
 
+/* One stand-alone sub-controller per QP slot (the reference's per-object
+ * DistributedController API; the NerveCenter path is cmpc_iterate /
+ * cmpc_observe_apply):
+ *   cmpc_get_input  DistributedController::GetInput(&du, du_last)
+ *                   (include/distributed_controller.h:206-226): f_k = f + G du_last
+ *                   (ApplyOtherInput, distributed_solver.h:98-103) and one
+ *                   warm-started SolveQP; du_last: device, B*S*nVo doubles per
+ *                   slot, the other controllers' plans controller-major, then
+ *                   move, then input (nerve_center.h:283-285); NULL for a full
+ *                   (centralized, nVo = 0) controller: SolveQP(qp_, u_old_).
+ *                   Results through cmpc_download (du, status, nwsr); flags as
+ *                   cmpc_iterate (CMPC_APPLY_MOVE: u_old += first move)
+ *   cmpc_update_u   DistributedController::UpdateU(du) (:145-152): ObserveAPriori
+ *                   (du, u_old_) and u_old_ += du with the caller's full input
+ *                   change du (device, B*S*nu_tot, the slot's input order);
+ *                   NerveCenter passes only the own inputs, the others zero
+ *                   (nerve_center.h:323-328; cmpc_observe_apply does that)
+ * The _host variants take host arrays (staged on the context's stream). */
+int cmpc_get_input(cmpc_ctx* ctx, const double* du_last, uint32_t flags);
+int cmpc_get_input_host(cmpc_ctx* ctx, const double* du_last, uint32_t flags);
+int cmpc_update_u(cmpc_ctx* ctx, const double* du_full);
+int cmpc_update_u_host(cmpc_ctx* ctx, const double* du_full);
+
 /* Sub-controller-sharded cooperative iteration.
  * S_total sub-controllers per scenario are spread over the ranks, S_local of
  * them on this context (QP slot q = scenario * S_local + local index; global

@@ -8,6 +8,9 @@
 //   ControllerInterface<System>::GetNextInput(y)      include/controller_interface.h:46
 //   NerveCenter ctor (controllers, n_solver_iterations) include/nerve_center.h:89-95
 //   DistributedController(sys, constraints, M)         include/distributed_controller.h:126-128
+//   DistributedController::{Initialize, SetWeights, SetOutputReference,
+//     UpdateU, GenerateInitialQP, GetInput, GetStateEstimate}
+//                                                       include/distributed_controller.h:131-191
 //   NerveCenter::Initialize(x, u, u_full, y, dx)      include/nerve_center.h:98-104
 //   NerveCenter::SetWeights(uwt, ywt)                 include/nerve_center.h:107-110
 //   NerveCenter::SetWeights(uwt, {ywt_s})             include/nerve_center.h:113-116
@@ -34,6 +37,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <memory>
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
@@ -193,21 +197,144 @@ struct InputConstraints {
   bool use_rate_constraints = false;
 };
 
+// The C ABI dimensions of sub-controller s of spec (delays in its own input
+// order) for B scenarios and S sub-controllers per scenario.
+inline cmpc_dims SubControllerDims(const ControllerSpec& spec, int s, int S, int B) {
+  cmpc_dims d{};
+  d.ns = spec.ns;
+  d.ndist = spec.ndist;
+  d.nu_tot = spec.nu_tot;
+  d.nu = spec.nu;
+  d.ny = spec.ny;
+  d.p = spec.p;
+  d.m = spec.m;
+  d.S = S;
+  d.B = B;
+  for (int c = 0; c < spec.nu_tot; ++c) d.delay[c] = spec.delays[spec.input_order[s][c]];
+  return d;
+}
+
 // DistributedController<AugLinSys, ...>(sys, constraints, M)
-// (include/distributed_controller.h:126-128): the constructor arguments of
-// one sub-controller.  Its template arguments (plant, index maps, delays,
-// p, m) are the ControllerSpec; M is the (ns + ndist) x n_outputs observer
-// gain, row-major (empty: no device observer, see NerveCenter).
+// (include/distributed_controller.h:126-128).  Two uses, as in the reference:
+//  - the constructor arguments of one sub-controller of a NerveCenter
+//    (DistributedController(constraints, M)); its template arguments (plant,
+//    index maps, delays, p, m) are the ControllerSpec; M is the
+//    (ns + ndist) x n_outputs observer gain, row-major (empty: no device
+//    observer, see NerveCenter);
+//  - a stand-alone sub-controller (DistributedController(spec, s, constraints,
+//    M)): sub-controller s of spec on its own one-slot device context, driven
+//    through the reference's member functions (distributed_controller.h:131-191)
+//    by a harness that runs the cooperative iteration itself.  Vectors are in
+//    the reference's orders: FullControlInput = this controller's input order
+//    (own inputs first), Output / Input = the plant's.
 class DistributedController {
  public:
   explicit DistributedController(InputConstraints constraints, std::vector<double> M = {})
       : constraints_(std::move(constraints)), M_(std::move(M)) {}
+  DistributedController(const ControllerSpec& spec, int s, InputConstraints constraints,
+                        std::vector<double> M, int device = 0)
+      : constraints_(std::move(constraints)), M_(std::move(M)), dev_(std::make_shared<Device>()) {
+    if (s < 0 || s >= spec.S()) throw Error("DistributedController: bad sub-controller index");
+    if (static_cast<int>(M_.size()) != (spec.ns + spec.ndist) * spec.n_outputs)
+      throw Error("DistributedController: M must be (ns + ndist) x n_outputs");
+    for (const auto* v : {&constraints_.lower_bound, &constraints_.upper_bound,
+                          &constraints_.lower_rate_bound, &constraints_.upper_rate_bound})
+      if (static_cast<int>(v->size()) != spec.nu) throw Error("InputConstraints: nu values per bound");
+    dev_->spec = spec;
+    dev_->s = s;
+    cmpc_dims d = SubControllerDims(spec, s, 1, 1);
+    Check(cmpc_create(&dev_->ctx, &d, device), "cmpc_create");
+    Check(cmpc_get_layout(dev_->ctx, &dev_->L), "cmpc_get_layout");
+    Check(cmpc_set_constraints(dev_->ctx, 0, constraints_.lower_bound.data(), constraints_.upper_bound.data(),
+                               constraints_.lower_rate_bound.data(), constraints_.upper_rate_bound.data()),
+          "cmpc_set_constraints");
+    Check(cmpc_set_observer(dev_->ctx, 0, spec.n_outputs, M_.data()), "cmpc_set_observer");
+  }
   const InputConstraints& constraints() const { return constraints_; }
   const std::vector<double>& observer_matrix() const { return M_; }
 
+  /// Initialize(x_init, u_init, full_u_old, y_init, dx_init)
+  /// (distributed_controller.cc:27-67): x_init ns, u_init nu_tot (this
+  /// controller's order), full_u_old n_inputs, y_init n_outputs, dx_init the
+  /// AugmentedState (ntot) or null for zero.  Builds the QP at x_init and runs
+  /// InitializeQPProblem.
+  void Initialize(const double* x_init, const double* u_init, const double* full_u_old,
+                  const double* y_init, const double* dx_init = nullptr) {
+    Device& D = dev();
+    const std::vector<double> du0(D.L.nV, 0.0);
+    const uint32_t ws0 = 0;
+    Check(cmpc_set_state(D.ctx, u_init, du0.data(), &ws0), "cmpc_set_state");
+    Check(cmpc_observer_init_host(D.ctx, static_cast<int>(D.spec.plant), 1.0, 1.0, 0.05,
+                                  D.spec.input_order[D.s].data(), D.spec.out_idx[D.s].data(), x_init,
+                                  full_u_old, y_init, dx_init),
+          "cmpc_observer_init_host");
+    Check(cmpc_build(D.ctx), "cmpc_build");
+    Check(cmpc_init_warmstart(D.ctx), "cmpc_init_warmstart");
+    Check(cmpc_synchronize(D.ctx), "cmpc_synchronize");
+  }
+  /// SetWeights(uwt, ywt) (:136-138): uwt nu x nu, ywt ny x ny, row-major.
+  void SetWeights(const double* uwt, const double* ywt) {
+    Check(cmpc_set_weights(dev().ctx, 0, uwt, ywt), "cmpc_set_weights");
+  }
+  /// SetOutputReference(y_ref) (:141-143): p x ny, prediction-major.
+  void SetOutputReference(const double* y_ref) {
+    Check(cmpc_set_reference(dev().ctx, 0, y_ref), "cmpc_set_reference");
+  }
+  /// UpdateU(du) (:146-152): ObserveAPriori(du, u_old_), u_old_ += du; du is
+  /// nu_tot in this controller's order.
+  void UpdateU(const double* du) { Check(cmpc_update_u_host(dev().ctx, du), "cmpc_update_u_host"); }
+  /// GenerateInitialQP(y, full_u_old) (distributed_controller.cc:72-108):
+  /// a-posteriori observer update, linearisation at the estimate, the QP.
+  void GenerateInitialQP(const double* y, const double* full_u_old) {
+    Device& D = dev();
+    Check(cmpc_observe_step_host(D.ctx, full_u_old, y), "cmpc_observe_step_host");
+    Check(cmpc_build(D.ctx), "cmpc_build");
+  }
+  /// GetInput(&u_solution, du_last) (:173-183, :206-226): the QP with the other
+  /// controllers' plans du_last (m * (nu_tot - nu) values, controller-major;
+  /// ignored by a centralized controller), warm-started; u_solution gets nV
+  /// moves (zero on a solver failure, as the reference).
+  void GetInput(double* u_solution, const double* du_last) {
+    Device& D = dev();
+    Check(cmpc_get_input_host(D.ctx, D.L.nVo > 0 ? du_last : nullptr, 0u), "cmpc_get_input_host");
+    Check(cmpc_download(D.ctx, u_solution, &D.status, &D.nwsr), "cmpc_download");
+  }
+  /// GetStateEstimate() (:186-191): the observer's x_ (ns values).
+  std::vector<double> GetStateEstimate() {
+    std::vector<double> x(dev().spec.ns);
+    GetStateEstimate(x.data());
+    return x;
+  }
+  void GetStateEstimate(double* x_out) {
+    Device& D = dev();
+    std::vector<double> row(static_cast<size_t>(cmpc_observer_len(D.ctx)));
+    Check(cmpc_get_observer_state(D.ctx, row.data()), "cmpc_get_observer_state");
+    for (int i = 0; i < D.spec.ns; ++i) x_out[i] = row[i];
+  }
+  /// status word and working-set change count of the last GetInput
+  int last_status() { return dev().status; }
+  int last_nwsr() { return dev().nwsr; }
+  cmpc_ctx* handle() { return dev().ctx; }
+
  private:
+  struct Device {
+    ControllerSpec spec;
+    int s = 0;
+    cmpc_ctx* ctx = nullptr;
+    cmpc_layout L{};
+    int32_t status = 0, nwsr = 0;
+    ~Device() {
+      if (ctx) cmpc_destroy(ctx);
+    }
+  };
+  Device& dev() {
+    if (!dev_) throw Error("DistributedController: constructed as NerveCenter arguments; use "
+                           "DistributedController(spec, s, constraints, M) to drive it directly");
+    return *dev_;
+  }
   InputConstraints constraints_;
   std::vector<double> M_;
+  std::shared_ptr<Device> dev_;
 };
 
 // ControllerInterface<System> (include/controller_interface.h:18-50): the
@@ -227,23 +354,12 @@ class NerveCenter : public ControllerInterface {
  public:
   NerveCenter(const ControllerSpec& spec, int n_solver_iterations, int device = 0)
       : spec_(spec), K_(n_solver_iterations) {
-    d_ = cmpc_dims{};
-    d_.ns = spec.ns;
-    d_.ndist = spec.ndist;
-    d_.nu_tot = spec.nu_tot;
-    d_.nu = spec.nu;
-    d_.ny = spec.ny;
-    d_.p = spec.p;
-    d_.m = spec.m;
-    d_.S = spec.S();
-    d_.B = 1;
+    d_ = SubControllerDims(spec, 0, spec.S(), 1);
     // delays in each sub-controller's input order; the ABI shares them
-    for (int c = 0; c < spec.nu_tot; ++c) {
-      d_.delay[c] = spec.delays[spec.input_order[0][c]];
+    for (int c = 0; c < spec.nu_tot; ++c)
       for (int s = 1; s < spec.S(); ++s)
         if (spec.delays[spec.input_order[s][c]] != d_.delay[c])
           throw Error("sub-controllers with different delay orderings");
-    }
     Check(cmpc_create(&ctx_, &d_, device), "cmpc_create");
     Check(cmpc_get_layout(ctx_, &L_), "cmpc_get_layout");
     u_old_.assign(spec.nu_tot, 0.0);
@@ -386,7 +502,12 @@ class NerveCenter : public ControllerInterface {
   }
 
   /// NerveCenter::GetNextInputWithTiming(y, n_timing_iterations, time_out)
-  /// (nerve_center.h:134-182), the observer on the device.
+  /// (nerve_center.h:134-182), the observer on the device.  Timing as the
+  /// reference's cpu_timer: it runs from the call to the end of the step and
+  /// is stopped from the start of Jacobi iteration n_timing_iterations to the
+  /// end of the loop (if 0 <= n_timing_iterations < K), so UpdateUOld and
+  /// SendUHelper (here the download and the observer's a-priori update) are
+  /// inside the time.
   std::vector<double> GetNextInputWithTiming(const double* y, int n_timing_iterations,
                                              int64_t* time_out_ns = nullptr) {
     if (!observer_on()) throw Error("GetNextInput(y) needs SetObserver for every sub-controller");
@@ -396,11 +517,12 @@ class NerveCenter : public ControllerInterface {
     // ObserveAPosteriori + Update at each sub-controller's estimate
     Check(cmpc_observe_step_host(ctx_, u_full.data(), y), "cmpc_observe_step_host");
     Check(cmpc_build(ctx_), "cmpc_build");
-    const int64_t timed = Iterate(n_timing_iterations, 0u, t0);
+    const int64_t stopped = Iterate(n_timing_iterations, 0u);
     Download();
     // UpdateU of every sub-controller (observer a priori + its u_old_)
     Check(cmpc_observe_apply(ctx_), "cmpc_observe_apply");
-    return Finish(timed, t0, time_out_ns);
+    if (time_out_ns) Check(cmpc_synchronize(ctx_), "cmpc_synchronize");  // the a-priori update is timed
+    return Finish(stopped, t0, time_out_ns);
   }
 
   /// ControllerInterface::GetNextInput with the observer's estimate supplied.
@@ -409,10 +531,10 @@ class NerveCenter : public ControllerInterface {
     return GetNextInputWithTiming(y, x_hat, dx_aug);
   }
 
-  /// GetNextInputWithTiming: if 0 <= n_timing_iterations < K, the wall time of
-  /// QP generation + the first n_timing_iterations Jacobi iterations is
-  /// returned in *time_out_ns (as the reference's cpu_timer); otherwise the
-  /// whole step is timed.
+  /// GetNextInputWithTiming: the wall time of the step without Jacobi
+  /// iterations n_timing_iterations .. K-1 (if 0 <= n_timing_iterations < K)
+  /// is returned in *time_out_ns, as the reference's cpu_timer
+  /// (nerve_center.h:137-179).
   std::vector<double> GetNextInputWithTiming(const double* y, const double* x_hat,
                                              const double* dx_aug = nullptr,
                                              int n_timing_iterations = -1,
@@ -423,9 +545,18 @@ class NerveCenter : public ControllerInterface {
     FillRecords(x_hat, u_full.data(), dx_aug, y);
     Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
     Check(cmpc_build(ctx_), "cmpc_build");
-    const int64_t timed = Iterate(n_timing_iterations, CMPC_APPLY_MOVE, t0);
+    const int64_t stopped = Iterate(n_timing_iterations, CMPC_APPLY_MOVE);
     Download();
-    return Finish(timed, t0, time_out_ns);
+    return Finish(stopped, t0, time_out_ns);
+  }
+
+  /// Sub-controller s's observer estimate x_ (ns values; the device observer,
+  /// DistributedController::GetStateEstimate of its s-th controller).
+  std::vector<double> GetStateEstimate(int s) {
+    std::vector<double> rows(static_cast<size_t>(spec_.S()) * cmpc_observer_len(ctx_));
+    Check(cmpc_get_observer_state(ctx_, rows.data()), "cmpc_get_observer_state");
+    const double* r = rows.data() + static_cast<size_t>(s) * cmpc_observer_len(ctx_);
+    return std::vector<double>(r, r + spec_.ns);
   }
 
   /// Move plans (S x nV), QP status words and working-set change counts of the last step.
@@ -434,21 +565,21 @@ class NerveCenter : public ControllerInterface {
   const std::vector<int32_t>& last_nwsr() const { return nwsr_; }
 
  private:
-  // K Jacobi iterations, the last with `last_flags`; if 0 <= n < K, the wall
-  // time up to iteration n is returned (the reference's stopped cpu_timer)
-  int64_t Iterate(int n_timing_iterations, uint32_t last_flags,
-                  std::chrono::steady_clock::time_point t0) {
-    int64_t timed = -1;
+  // K Jacobi iterations, the last with `last_flags`.  If 0 <= n < K, the
+  // reference stops its timer before iteration n and resumes it after the
+  // loop (nerve_center.h:151,158): returns that stopped span (ns), else 0.
+  int64_t Iterate(int n_timing_iterations, uint32_t last_flags) {
     if (n_timing_iterations >= 0 && n_timing_iterations < K_) {
       Check(cmpc_iterate(ctx_, n_timing_iterations, 0u), "cmpc_iterate");
       Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
-      timed = std::chrono::duration_cast<std::chrono::nanoseconds>(
-                  std::chrono::steady_clock::now() - t0).count();
+      const auto stop = std::chrono::steady_clock::now();
       Check(cmpc_iterate(ctx_, K_ - n_timing_iterations, last_flags), "cmpc_iterate");
-    } else {
-      Check(cmpc_iterate(ctx_, K_, last_flags), "cmpc_iterate");
+      Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
+      return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - stop)
+          .count();
     }
-    return timed;
+    Check(cmpc_iterate(ctx_, K_, last_flags), "cmpc_iterate");
+    return 0;
   }
   void Download() {
     du_.resize(static_cast<size_t>(spec_.S()) * spec_.nV());
@@ -456,15 +587,16 @@ class NerveCenter : public ControllerInterface {
     nwsr_.resize(spec_.S());
     Check(cmpc_download(ctx_, du_.data(), status_.data(), nwsr_.data()), "cmpc_download");
   }
-  // UpdateUOld (include/nerve_center.h:313-319): apply each first move
-  std::vector<double> Finish(int64_t timed, std::chrono::steady_clock::time_point t0,
+  // UpdateUOld (include/nerve_center.h:313-319): apply each first move; the
+  // step's time without the stopped span
+  std::vector<double> Finish(int64_t stopped, std::chrono::steady_clock::time_point t0,
                              int64_t* time_out_ns) {
     for (int s = 0; s < spec_.S(); ++s)
       for (int c = 0; c < spec_.nu; ++c) u_old_[spec_.input_order[s][c]] += du_[s * spec_.nV() + c];
     if (time_out_ns)
-      *time_out_ns = timed >= 0 ? timed
-                                : std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                      std::chrono::steady_clock::now() - t0).count();
+      *time_out_ns =
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() -
+          stopped;
     return u_old_;
   }
 

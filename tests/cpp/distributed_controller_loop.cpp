@@ -1,0 +1,150 @@
+// The reference's per-object DistributedController API
+// (include/distributed_controller.h:131-191) driven the way NerveCenter drives
+// it (include/nerve_center.h:134-182, 276-328), against cmpc::NerveCenter on
+// the same inputs.  Each sub-controller is a stand-alone
+// cmpc::DistributedController on its own one-slot device context; this
+// program runs the cooperative Jacobi loop on the host:
+//   GenerateInitialQP(y, u_full_old) per controller,
+//   K x { GetInput(&du_s, du_prev without its own segment) },
+//   UpdateUOld, SendUHelper: UpdateU(du with only the own inputs set),
+// and checks, step by step, that the applied inputs, the move plans, the QP
+// status words and every controller's GetStateEstimate equal NerveCenter's
+// bit for bit.
+//
+// usage: distributed_controller_loop <setup-file> <par|ser> <cent|coop|ncoop> [p] [steps]
+// Prints one line per step; exit 0 if every step matched, 3 otherwise.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "cmpc/nerve_center.hpp"
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    std::fprintf(stderr, "usage: %s <setup-file> <par|ser> <cent|coop|ncoop> [p] [steps]\n", argv[0]);
+    return 2;
+  }
+  try {
+    using namespace cmpc;
+    const PlantType plant = std::strcmp(argv[2], "ser") == 0 ? PlantType::Serial : PlantType::Parallel;
+    const ControllerType type = std::strcmp(argv[3], "cent") == 0 ? ControllerType::Centralized
+                                : std::strcmp(argv[3], "ncoop") == 0 ? ControllerType::NonCooperative
+                                                                    : ControllerType::Cooperative;
+    const int p = argc > 4 ? std::atoi(argv[4]) : 100;
+    const int steps = argc > 5 ? std::atoi(argv[5]) : 6;
+    const ControllerSpec spec = ControllerSpec::Reference(plant, type, p);
+    const SetupFile setup = SetupFile::Read(argv[1]);
+    const int S = spec.S(), nV = spec.nV(), nu = spec.nu, nut = spec.nu_tot, K = setup.n_iterations;
+
+    // observer gain: 0.5 on the disturbance states (the innovation moves them)
+    const int nobs = spec.ns + spec.ndist;
+    std::vector<double> M(static_cast<size_t>(nobs) * spec.n_outputs, 0.0);
+    for (int o = 0; o < spec.ndist && o < spec.n_outputs; ++o) M[(spec.ns + o) * spec.n_outputs + o] = 0.5;
+    auto sub = [&](const std::vector<double>& v, int s) {
+      std::vector<double> r(nu);
+      for (int c = 0; c < nu; ++c) r[c] = static_cast<int>(v.size()) == nu ? v[c] : v[spec.input_order[s][c]];
+      return r;
+    };
+    std::vector<InputConstraints> ics(S);
+    for (int s = 0; s < S; ++s) {
+      ics[s].lower_bound = sub(setup.lower, s);
+      ics[s].upper_bound = sub(setup.upper, s);
+      ics[s].lower_rate_bound = sub(setup.rate_lower, s);
+      ics[s].upper_rate_bound = sub(setup.rate_upper, s);
+    }
+    // (a) NerveCenter over the sub-controllers
+    std::vector<DistributedController> args;
+    for (int s = 0; s < S; ++s) args.emplace_back(ics[s], M);
+    NerveCenter nc(spec, args, K);
+    // (b) the same sub-controllers, stand-alone
+    std::vector<DistributedController> ctrl;
+    for (int s = 0; s < S; ++s) ctrl.emplace_back(spec, s, ics[s], M);
+
+    // weights, output reference: NerveCenter takes the plant-wide arrays,
+    // each controller its own block (NerveCenter::SetWeights/SetOutputReference)
+    const int blk = spec.ny * spec.ny;
+    std::vector<const double*> ywt(S);
+    for (int s = 0; s < S; ++s)
+      ywt[s] = setup.ywt.data() + (static_cast<int>(setup.ywt.size()) == blk * S ? s * blk : 0);
+    nc.SetWeights(setup.uwt.data(), ywt);
+    std::vector<double> y_ref(static_cast<size_t>(p) * spec.n_outputs);
+    for (int i = 0; i < p; ++i)
+      for (int o = 0; o < spec.n_outputs; ++o) y_ref[i * spec.n_outputs + o] = setup.yref[o];
+    nc.SetOutputReference(y_ref.data());
+    for (int s = 0; s < S; ++s) {
+      std::vector<double> uw(nu * nu), yr(static_cast<size_t>(p) * spec.ny);
+      for (int a = 0; a < nu; ++a)
+        for (int b = 0; b < nu; ++b) uw[a * nu + b] = setup.uwt[spec.input_order[s][a] * nut + spec.input_order[s][b]];
+      for (int i = 0; i < p; ++i)
+        for (int o = 0; o < spec.ny; ++o) yr[i * spec.ny + o] = y_ref[i * spec.n_outputs + spec.out_idx[s][o]];
+      ctrl[s].SetWeights(uw.data(), ywt[s]);
+      ctrl[s].SetOutputReference(yr.data());
+    }
+
+    std::vector<double> x0(spec.ns), u_off(spec.n_inputs), y0(spec.n_outputs);
+    Check(cmpc_plant_default(static_cast<int>(plant), x0.data(), u_off.data()), "cmpc_plant_default");
+    Check(cmpc_plant_output(static_cast<int>(plant), x0.data(), y0.data()), "cmpc_plant_output");
+    const std::vector<double> u0(nut, 0.0);
+    nc.Initialize(x0.data(), u0.data(), u_off.data(), y0.data());
+    for (int s = 0; s < S; ++s) ctrl[s].Initialize(x0.data(), u0.data(), u_off.data(), y0.data());
+
+    // NerveCenter's own state for the hand-driven loop (nerve_center.h:71-75)
+    std::vector<double> u_old(nut, 0.0), du_old(static_cast<size_t>(S) * nV, 0.0);
+    bool all_equal = true;
+    for (int k = 0; k < steps; ++k) {
+      std::vector<double> y(y0);
+      for (int o = 0; o < spec.n_outputs; ++o) y[o] = y0[o] * (1.0 + 2e-3 * std::sin(1.3 * k + o));
+      // (a)
+      const std::vector<double> u_nc = nc.GetNextInput(y.data());
+      // (b) GetNextInputWithTiming's body with the per-object calls
+      std::vector<double> u_full(u_off);
+      for (int c = 0; c < nut; ++c) u_full[spec.plant_input_index[c]] += u_old[c];
+      for (int s = 0; s < S; ++s) ctrl[s].GenerateInitialQP(y.data(), u_full.data());
+      std::vector<double> du_prev(du_old), du_new(du_old.size());
+      std::vector<int> status(S, 0);
+      for (int i = 0; i < K; ++i) {
+        for (int s = 0; s < S; ++s) {
+          std::vector<double> du_last;  // the others' plans, controller-major (:283-285)
+          for (int s2 = 0; s2 < S; ++s2)
+            if (s2 != s) du_last.insert(du_last.end(), du_prev.begin() + s2 * nV, du_prev.begin() + (s2 + 1) * nV);
+          ctrl[s].GetInput(du_new.data() + s * nV, du_last.empty() ? nullptr : du_last.data());
+          status[s] = ctrl[s].last_status();
+        }
+        du_prev = du_new;
+      }
+      du_old = du_prev;
+      // UpdateUOld, then SendUHelper: each controller gets du with only its own
+      // inputs set (nerve_center.h:313-328)
+      std::vector<double> du_applied(nut, 0.0);
+      for (int s = 0; s < S; ++s)
+        for (int c = 0; c < nu; ++c) {
+          u_old[spec.input_order[s][c]] += du_old[s * nV + c];
+          du_applied[spec.input_order[s][c]] = du_old[s * nV + c];
+        }
+      for (int s = 0; s < S; ++s) {
+        std::vector<double> du_s(nut, 0.0);
+        for (int c = 0; c < nu; ++c) du_s[c] = du_applied[spec.input_order[s][c]];
+        ctrl[s].UpdateU(du_s.data());
+      }
+      // compare
+      bool eq = u_nc == u_old && nc.last_plans() == du_old;
+      for (int s = 0; s < S; ++s) {
+        eq = eq && nc.last_status()[s] == status[s];
+        eq = eq && nc.GetStateEstimate(s) == ctrl[s].GetStateEstimate();
+      }
+      double dmax = 0;
+      for (int c = 0; c < nut; ++c) dmax = std::fmax(dmax, std::fabs(u_nc[c] - u_old[c]));
+      std::printf("step %d: u", k);
+      for (double v : u_old) std::printf(" %.9g", v);
+      std::printf("  status");
+      for (int v : status) std::printf(" %d", v);
+      std::printf("  %s (max |du| %.3g)\n", eq ? "equal" : "DIFFERENT", dmax);
+      all_equal = all_equal && eq;
+    }
+    return all_equal ? 0 : 3;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return 1;
+  }
+}

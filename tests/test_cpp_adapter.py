@@ -181,3 +181,39 @@ def test_gpu_cpp_harness_timed_prefix_keeps_trajectory(n_timing, tmp_path):
     assert len(recs) == 1200
     for k, rec in enumerate(recs):
         assert six(rec["u"].split()) == six(ur[k]), (k, rec["u"], ur[k])
+
+
+LOOP = os.path.join(HERE, "cpp", "distributed_controller_loop")
+
+
+def test_controller_loop_builds_and_fails_loudly_without_device(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "cpp"), "distributed_controller_loop"])
+    cfg, _, _, g = GC.case("coop-par")
+    setup = tmp_path / "setup-coop-par"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([LOOP, str(setup), "par", "coop"], capture_output=True, text=True)
+    assert r.returncode == 1 and "error: cmpc_create" in r.stderr, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent-par", "coop-par", "ncoop-par", "cent-ser", "coop-ser", "ncoop-ser"])
+def test_gpu_distributed_controller_api_matches_nerve_center(name, tmp_path):
+    """The per-object DistributedController API (Initialize, SetWeights,
+    SetOutputReference, GenerateInitialQP, GetInput, UpdateU,
+    GetStateEstimate; distributed_controller.h:131-191), each sub-controller
+    on its own one-slot context and the Jacobi loop run on the host as
+    NerveCenter runs it, equals cmpc::NerveCenter bit for bit over 6 steps
+    with a moving measured output (applied inputs, plans, statuses, state
+    estimates)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "cpp"), "distributed_controller_loop"])
+    cfg, _, _, g = GC.case(name)
+    ctype, plant = name.split("-")
+    setup = tmp_path / f"setup-{name}"
+    write_setup(setup, g, cfg.ny, cfg.S)
+    r = subprocess.run([LOOP, str(setup), plant, ctype, "50", "6"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("step ")]
+    assert len(lines) == 6 and all(" equal " in l for l in lines), r.stdout

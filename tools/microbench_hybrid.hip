@@ -104,7 +104,7 @@ __device__ __forceinline__ void chain_gather(double* aP, double& aS, const doubl
 }
 
 template <int V>
-__global__ __launch_bounds__(256) void kern(const double* __restrict__ in, double* out, long long* clk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void kern(const double* __restrict__ in, double* out, long long* clk) {
   const int lane = threadIdx.x & 63;
   long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   double res = 0;
@@ -138,6 +138,67 @@ __global__ __launch_bounds__(256) void kern(const double* __restrict__ in, doubl
         }
       }
       res += acc[0] + acc[1] + acc[2] + acc[3] + pP[0] + pP[1] + pP[2] + pS;
+    } else if constexpr (V == 4) {
+      // V4 (round 3): P^T chain on MFMA with A^4 blocking: P^T_{r+4} = (A^4)^T P^T_r
+      // (3 row tiles x 3 k = 9), Markov of the block's 4 steps from P^T_r and
+      // (A^k B)^T (4 x 3 = 12), Gram over k = 4 steps x 3 outputs (3 col tiles
+      // x 3 k-chunks = 9); free response on DPP (13 per step, 2 chains), the
+      // running sums as 1 VALU add per step; the column hand-off through LDS
+      // (8 writes + 12 reads per block per lane)
+      __shared__ double lds[4][64 * 8];
+      double* wl = lds[threadIdx.x >> 6];
+      double A4T[9], PT[3], AkB[12], m[13], S = 0.0;
+      for (int i = 0; i < 9; ++i) A4T[i] = ld(i) * 0.3;
+      for (int i = 0; i < 3; ++i) PT[i] = ld(9 + i);
+      for (int i = 0; i < 12; ++i) AkB[i] = ld(12 + i) * 0.3;
+      for (int i = 0; i < 13; ++i) m[i] = ld(24 + i) * 0.3;
+      double pS = ld(37);
+      double G[3] = {0, 0, 0};
+#pragma unroll 1
+      for (int b = 0; b < NBLK; ++b) {
+        double Mk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // Markov of step 4b + k: (A^k B)^T P^T_r
+          double d = M4(AkB[k * 3 + 0], PT[0], 0.0);
+          d = M4(AkB[k * 3 + 1], PT[1], d);
+          Mk[k] = M4(AkB[k * 3 + 2], PT[2], d);
+        }
+        double Pn[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          double d = M4(A4T[i * 3 + 0], PT[0], 0.0);
+          d = M4(A4T[i * 3 + 1], PT[1], d);
+          Pn[i] = M4(A4T[i * 3 + 2], PT[2], d);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          S = S + Mk[k];                       // running sum (move-1 columns)
+          wl[(k * 2 + 0) * 64 + lane] = Mk[k];  // hand-off writes
+          wl[(k * 2 + 1) * 64 + lane] = S;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          double s0 = pS * 0.5, s1 = 0.0;
+          free_resp(s0, s1, pS, m);
+          pS = s0 + s1;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        // column reads (A: own columns over 3 k-chunks, B: 3 tiles x 3 chunks)
+        double Ac[3], Bc[9];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Ac[c] = wl[((c * 5 + 1) & 7) * 64 + (lane ^ (c + 1))];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) Bc[t] = wl[((t * 3 + 2) & 7) * 64 + (lane ^ (t + 5))];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {  // Gram: 3 column tiles x 3 k-chunks
+          double d = M4(Ac[0], Bc[t * 3 + 0], G[t]);
+          d = M4(Ac[1], Bc[t * 3 + 1], d);
+          G[t] = M4(Ac[2], Bc[t * 3 + 2], d);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) PT[i] = Pn[i];
+      }
+      res += pS + S + G[0] + G[1] + G[2] + PT[0] + PT[1] + PT[2];
     } else {
       // MFMA tiles: A4T[9] constants, T[9] chain state, Bt[3] constants
       double A4T[9], T[9], Bt[3], m[13], acc[4] = {0, 0, 0, 0}, cv[3] = {0, 0, 0}, Mk[3] = {0, 0, 0};
@@ -248,6 +309,7 @@ int main() {
     timeit<3>("V3 dpp ilp", w, in, out, clk);
     timeit<1>("V1 hybrid", w, in, out, clk);
     timeit<2>("V2 mfma", w, in, out, clk);
+    timeit<4>("V4 mfma-a4", w, in, out, clk);
   }
   return 0;
 }
