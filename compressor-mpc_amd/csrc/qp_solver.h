@@ -125,14 +125,29 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
 // Working set: slots 0..K-1 sorted by constraint index j, each with its
 // normal, bound beta and multiplier.  h_a = Hinv * normal_a is recomputed
 // where it is used (registers: the solve kernel runs at 2 waves/SIMD).
-template <int N>
+// SN (store normals): the explicit normal vectors are kept per slot (N <= 6);
+// for larger N they are rebuilt from (j, side) where they are used
+// (Qp::normal, the same vector bit for bit), which frees 2 N^2 registers per
+// working set: the centralized nV = 8 solve then needs no scratch.
+template <int N, bool SN = (N <= 6)>
 struct WSet {
   int K;
   int j[N], side[N];
   double lam[N];
-  double nrm[N][N], bta[N];
+  double nrm[SN ? N : 1][N], bta[N];
   double L[N][N], D[N];
 };
+
+// the normal of slot a (stored, or rebuilt from its constraint index)
+template <int N, bool SN, class Q>
+CMPC_HD void wset_normal(const Q& q, const WSet<N, SN>& W, int a, double (&n)[N]) {
+  if constexpr (SN) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) n[c] = W.nrm[a][c];
+  } else {
+    q.normal(W.j[a], W.side[a], n);
+  }
+}
 
 // LDL' of the leading K x K block of M (M symmetric); returns false on a
 // non-positive pivot.
@@ -191,17 +206,25 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
 }
 
 // (re)build h, M = N' Hinv N and its LDL' for the current working set
-template <int N, class Q>
-CMPC_HD bool wset_factor(const Q& q, WSet<N>& W) {
+template <int N, bool SN, class Q>
+CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
   double M[N][N];
 #pragma unroll
   for (int b = 0; b < N; ++b) {
     double hb[N];
-    if (b < W.K) q.hinv_n(W.nrm[b], hb);
+    if (b < W.K) {
+      double nb[N];
+      wset_normal(q, W, b, nb);
+      q.hinv_n(nb, hb);
+    }
 #pragma unroll
     for (int a = 0; a <= b; ++a) {
       double v = 0.0;
-      if (b < W.K) v = ndot<N>(W.nrm[a], hb);
+      if (b < W.K) {
+        double na[N];
+        wset_normal(q, W, a, na);
+        v = ndot<N>(na, hb);
+      }
       M[a][b] = v;
       M[b][a] = v;
     }
@@ -209,8 +232,8 @@ CMPC_HD bool wset_factor(const Q& q, WSet<N>& W) {
   return ldl_k<N>(W.K, M, W.L, W.D);
 }
 
-template <int N>
-CMPC_HD void wset_drop(WSet<N>& W, int a) {
+template <int N, bool SN>
+CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
 #pragma unroll
   for (int b = 0; b + 1 < N; ++b)
     if (b >= a && b + 1 < W.K) {
@@ -218,15 +241,17 @@ CMPC_HD void wset_drop(WSet<N>& W, int a) {
       W.side[b] = W.side[b + 1];
       W.lam[b] = W.lam[b + 1];
       W.bta[b] = W.bta[b + 1];
+      if constexpr (SN) {
 #pragma unroll
-      for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b + 1][c];
+        for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b + 1][c];
+      }
     }
   W.K--;
 }
 
 // sorted insert (phase B adds; the warm start fills slots directly)
-template <int N>
-CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam, const double (&n)[N], double bta) {
+template <int N, bool SN>
+CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double (&n)[N], double bta) {
   int pos = 0;
 #pragma unroll
   for (int b = 0; b < N; ++b)
@@ -238,8 +263,10 @@ CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam, const double (&n)
       W.side[b] = W.side[b - 1];
       W.lam[b] = W.lam[b - 1];
       W.bta[b] = W.bta[b - 1];
+      if constexpr (SN) {
 #pragma unroll
-      for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b - 1][c];
+        for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b - 1][c];
+      }
     }
 #pragma unroll
   for (int b = 0; b < N; ++b)
@@ -248,8 +275,10 @@ CMPC_HD void wset_add(WSet<N>& W, int j, int side, double lam, const double (&n)
       W.side[b] = side;
       W.lam[b] = lam;
       W.bta[b] = bta;
+      if constexpr (SN) {
 #pragma unroll
-      for (int c = 0; c < N; ++c) W.nrm[b][c] = n[c];
+        for (int c = 0; c < N; ++c) W.nrm[b][c] = n[c];
+      }
     }
   W.K++;
 }
@@ -311,6 +340,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
                          WSet<N>* wc = nullptr, uint32_t* wc_ws = nullptr) {
   WSet<N> Wl;
   WSet<N>& W = CACHE ? *wc : Wl;
+  constexpr bool SN = (N <= 6);
   const bool cached = CACHE && pd && *wc_ws == ws_in;
   bool fact_ok = cached;  // W.L, W.D are the factors of the current slots
   o.status = CMPC_QP_OK;
@@ -353,7 +383,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         W.j[a] = j;
         W.side[a] = sd;
         W.lam[a] = 0.0;
-        q.normal(j, sd, W.nrm[a]);
+        if constexpr (SN) q.normal(j, sd, W.nrm[a]);
         W.bta[a] = q.beta(j, sd);
         W.K = a + 1;
       }
@@ -370,8 +400,14 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     }
     double rhs[N];
 #pragma unroll
-    for (int a = 0; a < N; ++a)
-      rhs[a] = (a < W.K) ? W.bta[a] - ndot<N>(W.nrm[a], xu) : 0.0;
+    for (int a = 0; a < N; ++a) {
+      rhs[a] = 0.0;
+      if (a < W.K) {
+        double na[N];
+        wset_normal(q, W, a, na);
+        rhs[a] = W.bta[a] - ndot<N>(na, xu);
+      }
+    }
     ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
     if (CMPC_QP_ABL == 2) break;
     int worst = -1;
@@ -405,8 +441,9 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
 #pragma unroll
     for (int a = 0; a < N; ++a) {
       if (a < W.K) {
-        double ha[N];
-        q.hinv_n(W.nrm[a], ha);
+        double na[N], ha[N];
+        wset_normal(q, W, a, na);
+        q.hinv_n(na, ha);
 #pragma unroll
         for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
       }
@@ -456,15 +493,23 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       double hp[N], qv[N], rv[N], z[N];
       q.hinv_n(np_, hp);
 #pragma unroll
-      for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? ndot<N>(W.nrm[a], hp) : 0.0;
+      for (int a = 0; a < N; ++a) {
+        qv[a] = 0.0;
+        if (a < W.K) {
+          double na[N];
+          wset_normal(q, W, a, na);
+          qv[a] = ndot<N>(na, hp);
+        }
+      }
       ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
 #pragma unroll
       for (int r = 0; r < N; ++r) z[r] = hp[r];
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         if (a < W.K) {
-          double ha[N];
-          q.hinv_n(W.nrm[a], ha);
+          double na[N], ha[N];
+          wset_normal(q, W, a, na);
+          q.hinv_n(na, ha);
 #pragma unroll
           for (int r = 0; r < N; ++r) z[r] = z[r] - rv[a] * ha[r];
         }
