@@ -344,8 +344,11 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
   if (layout_of(dims, &L)) return -1;
   const cmpc_dims& d = *dims;
   if (64 % d.S != 0) return fail("S must divide the wavefront size (64)");
-  if (L.nuo != (d.S - 1) * d.nu)
-    return fail("nu_tot must equal S * nu (each sub-controller owns nu inputs)");
+  // S sub-controllers share the inputs (nu_tot = S nu), or S = 1 with
+  // nu < nu_tot: one stand-alone sub-controller whose other controllers'
+  // plans come with every cmpc_get_input (DistributedController::GetInput)
+  if (L.nuo != (d.S - 1) * d.nu && d.S != 1)
+    return fail("nu_tot must equal S * nu (each sub-controller owns nu inputs), or S = 1");
   if (L.nd > CMPC_ND_MAX) return fail("more than 4 delayed inputs");
   if (d.ns + d.nu_tot > 15) return fail("ns + nu_tot must be <= 15 (16-lane DPP rows)");
   if (d.m * d.nu_tot + 1 > 16) return fail("m * nu_tot + 1 must be <= 16 (gather lanes of a DPP row)");
@@ -1420,6 +1423,9 @@ int cmpc_init_warmstart(cmpc_ctx* c) {
 int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
   if (!c) return fail("null context");
   if (K < 0) return fail("K must be >= 0");
+  if (c->L.nuo != (c->d.S - 1) * c->d.nu)
+    return fail("cmpc_iterate: the other controllers' plans are not in this context (S = 1, nu < nu_tot): "
+                "use cmpc_get_input");
   if (ensure_cfg(c)) return -1;
   HIP_TRY(hipSetDevice(c->device));
   SolveParams P;
