@@ -168,7 +168,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   for (int k = 0; k < NDW; ++k)
     if (cl && k == kc && dlen[k] < pp) ysw = dlen[k];
   const int nseg = P.rows.nseg;
-  constexpr int NSEG = 2 * NDW;  // segment bounds come from the delayed inputs (D, p - D)
+  constexpr int NSEG = 5 * NDW;  // segment bounds come from the delayed inputs (D, p - D, ring wraps)
   int segb[NSEG];
 #pragma unroll
   for (int i = 0; i < NSEG; ++i) segb[i] = P.rows.seg[i];
@@ -191,6 +191,18 @@ void cmpc_build_rows_kernel(BuildParams P) {
                                           : dump;
   const int winc0 = (wdel && pp - dm > 0) ? NY : 0;
   const int wsw = (wdel && pp - dm > 0) ? pp - dm : -1;
+  // ring lines (RowsLayout::ring): the writer and each gather reader step back
+  // by the ring at their wrap steps (rows_layout.cpp, rows_ring_*_wrap)
+  int ringw = 0, ringr = 0;
+#pragma unroll
+  for (int c = 0; c < NUT; ++c) {
+    if (c == cm) ringw = P.rows.ring[c];
+    if (c == gc) ringr = P.rows.ring[c];
+  }
+  const int wwr = (wdel && ringw) ? ringw - (M - 1) : -1;
+  const int wback = ringw * NY;
+  const int rwr = (rdel && ringr) ? ringr + dg - (M - 1 - gk) : -1;
+  const int rback = ringr * NY;
   const bool tl = M > 1 && mk && dm == 0;  // ring writer: copies each group's last value to entry -1
   double* const tq = qlines + lom;
   // every lane stores each step (no exec-mask branches in the loop): lanes
@@ -305,12 +317,6 @@ void cmpc_build_rows_kernel(BuildParams P) {
     // every staged read is issued before the first table write below (LDS
     // operations of a wave execute in order)
     __builtin_amdgcn_sched_barrier(0);
-    // restore the zero areas the staging overwrote: the m - 1 history entries
-    // at the head of each delayed input's line, and the zero slots
-#pragma unroll
-    for (int c = 0; c < NUT; ++c)
-      if (P.delay[c] > 0 && j < (M - 1) * NY) qlines[P.rows.lo[c] + j] = 0.0;
-    for (int e = j; e < U * NY; e += 16) qlines[P.rows.zr_off + e] = 0.0;
 
     // C_hat = L_W' C_sel (ny x nobs): lane j computes column j of its QP
     double pP[NY];
@@ -368,6 +374,13 @@ void cmpc_build_rows_kernel(BuildParams P) {
       yp = wk + 3;
       yinc = 1;
     }
+    // restore the zero areas the staging (and the C_hat rows, which overlay
+    // the hand-off areas and were read above) overwrote: the m - 1 history
+    // entries at the head of each delayed input's line, and the zero slots
+#pragma unroll
+    for (int c = 0; c < NUT; ++c)
+      if (P.delay[c] > 0 && j < (M - 1) * NY) qlines[P.rows.lo[c] + j] = 0.0;
+    for (int e = j; e < U * NY; e += 16) qlines[P.rows.zr_off + e] = 0.0;
     // ring history before t = 0
     if (tl) {
 #pragma unroll
@@ -478,6 +491,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
         yp += yinc;
       }
       if (r == rsw) { rq = r_line; rinc = NY; }
+      if (r == rwr) rq -= rback;
+      if (r == wwr) wq -= wback;
       if (r == wsw) { wq = dump; winc = 0; }
       if (r == ysw) { yp = zeros; yinc = 0; }
     }

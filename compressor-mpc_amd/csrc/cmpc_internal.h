@@ -47,13 +47,19 @@ struct CfgOffsets {
 // input c at lo[c] a ring of U + 1 entries (undelayed) or m - 1 zero entries
 // + max(0, p - D_c) values (delayed); then a dump area, the free-response z
 // entries and a zero area (U entries each).
+// A delayed input's line is a ring of D + m entries when its p - D values
+// would need more (p > 2 D + 1): the writer and the two gather readers step
+// back by ring[c] entries at their wrap steps, which are loop segment bounds
+// too.  The C_hat rows overlay the hand-off areas: they are read in the
+// prologue only, before the zero areas are written.
 struct RowsLayout {
   int ok;                        // the row kernel can run these dimensions
   int lds_block, per_wave;
   int yl_off, yls, lw_off, uw_off;
   int LQ, lo[CMPC_MAX_INPUTS], dump_off, z_off, zr_off;
+  int ring[CMPC_MAX_INPUTS];      // entries of a wrapping delayed line, 0: a plain line
   int ch_off, w_off, WL;
-  int nseg, seg[2 * CMPC_MAX_INPUTS];  // ascending distinct D and p - D inside (0, p)
+  int nseg, seg[5 * CMPC_MAX_INPUTS];  // ascending distinct D, p - D and wrap steps inside (0, p)
 };
 
 struct BuildParams {

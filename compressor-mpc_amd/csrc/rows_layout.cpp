@@ -41,6 +41,14 @@ struct Pads {
 
 int up(int v, int a) { return (v + a - 1) / a * a; }
 
+// Wrap steps of a ring line of R entries (entry e holds the value of step
+// e - (m - 1), the first m - 1 entries start as history zeros): the writer of
+// step t stores entry m - 1 + t, so it steps back by R entries at t = R - m + 1;
+// the move-k reader reads entry (m - 1 - k) + s - D at step s >= D, so it steps
+// back at s = R + D - (m - 1 - k).
+int rows_ring_writer_wrap(int R, int M) { return R - (M - 1); }
+int rows_ring_reader_wrap(int R, int D, int M, int k) { return R + D - (M - 1 - k); }
+
 // The layout for given paddings (all offsets in doubles).  Returns the LDS
 // bytes per workgroup.
 size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, RowsLayout* R) {
@@ -51,7 +59,14 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
     const int c = pd.order[i];
     o += pd.pad_c[c];
     R->lo[c] = o;
-    o += ny * ((d.delay[c] == 0) ? U + 1 : (M - 1) + std::max(0, d.p - d.delay[c]));
+    int len = (d.delay[c] == 0) ? U + 1 : (M - 1) + std::max(0, d.p - d.delay[c]);
+    // a value written at step t is read until step t + D + m - 1: a ring of
+    // D + m entries holds every value still to be read (rows_ring_* below)
+    if (d.delay[c] > 0 && len > d.delay[c] + M) {
+      len = d.delay[c] + M;
+      R->ring[c] = len;
+    }
+    o += ny * len;
   }
   o += pd.dump;
   R->dump_off = o;
@@ -63,8 +78,11 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
   R->zr_off = o;
   o += U * ny;
   R->LQ = up(o, 2) + 2 * pd.LQ;
-  R->ch_off = 4 * R->LQ;
-  R->w_off = R->ch_off + 4 * ny * 16 + pd.w;
+  // the C_hat rows overlay the hand-off areas when those are large enough
+  // (build_rows.hip reads them in the prologue, before any area is written)
+  const int chs = 4 * ny * 16;
+  R->ch_off = (4 * R->LQ >= chs) ? 0 : 4 * R->LQ;
+  R->w_off = std::max(4 * R->LQ, R->ch_off + chs) + pd.w;
   // w lines: the carriers read entries 3 + r (r < p) until the segment r = D
   // of their input, then the zero slots (build_rows.hip): D + 3 entries
   int dmax = 0;
@@ -90,6 +108,10 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
     if (d.delay[c] > 0) {
       add(d.delay[c]);
       add(d.p - d.delay[c]);
+      if (R->ring[c]) {  // wrap steps: the writer's, and each move's gather reader's
+        add(rows_ring_writer_wrap(R->ring[c], M));
+        for (int k = 0; k < M; ++k) add(rows_ring_reader_wrap(R->ring[c], d.delay[c], M, k));
+      }
     }
   std::sort(R->seg, R->seg + R->nseg);
   return sizeof(double) * ((size_t)R->lds_block + (size_t)R->per_wave * CMPC_BUILD_WAVES);
@@ -117,7 +139,7 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
   const int NG = M * NUT + 1;
   const int wreg = R.lds_block + wave * R.per_wave;
   int rq[64], rinc[64], rline[64], rsw[64], wq[64], winc[64], wsw[64], dump[64], yp[64], yinc[64];
-  int zq[64], tq[64], ysw[64];
+  int zq[64], tq[64], ysw[64], rwr[64], wwr[64], rback[64], wback[64];
   int kdelay[CMPC_ND_MAX] = {0};  // delay of the k-th delayed input (ascending input index)
   for (int c = 0, k = 0; c < d.nu_tot && k < CMPC_ND_MAX; ++c)
     if (d.delay[c] > 0) kdelay[k++] = d.delay[c];
@@ -150,6 +172,11 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
                               : dump[lane];
     winc[lane] = (wdel && p - dm > 0) ? NY : 0;
     wsw[lane] = (wdel && p - dm > 0) ? p - dm : -1;
+    const int rgw = mk[lane] ? R.ring[cm] : 0, rgr = (gl && !zl) ? R.ring[gc] : 0;
+    wwr[lane] = (wdel && rgw) ? rows_ring_writer_wrap(rgw, M) : -1;
+    wback[lane] = rgw * NY;
+    rwr[lane] = (rdel && rgr) ? rows_ring_reader_wrap(rgr, dg, M, gk) : -1;
+    rback[lane] = rgr * NY;
     tl[lane] = M > 1 && mk[lane] && dm == 0;
     tq[lane] = ql + R.lo[cm];
     zq[lane] = ql + R.z_off + oo;
@@ -224,6 +251,8 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     }
     for (int l = 0; l < 64; ++l) {
       if (r == rsw[l]) { rq[l] = rline[l]; rinc[l] = NY; }
+      if (r == rwr[l]) rq[l] -= rback[l];
+      if (r == wwr[l]) wq[l] -= wback[l];
       if (r == wsw[l]) { wq[l] = dump[l]; winc[l] = 0; }
       if (r == ysw[l]) { yp[l] = 0; yinc[l] = 0; }  // the zero slots
     }

@@ -101,7 +101,8 @@ def test_library_fails_loudly_without_device():
 
 
 @pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "ncoop", 50), ("par", "cent", 50),
-                                           ("ser", "coop", 50), ("par", "coop", 20)])
+                                           ("ser", "coop", 50), ("par", "coop", 20), ("ser", "coop", 100),
+                                           ("ser", "cent", 100), ("par", "coop", 100)])
 def test_rows_lds_layout_search(plant, ctype, p):
     """The row build kernel's LDS layout (rows_layout.cpp): the bank-conflict
     model of its horizon loop is no worse than regions packed back to back
@@ -120,6 +121,11 @@ def test_rows_lds_layout_search(plant, ctype, p):
         assert 160 * 1024 // alloc >= 3  # the kernel runs three 4-wave workgroups per CU
     if (plant, ctype, p) == ("ser", "coop", 50):
         assert 160 * 1024 // alloc >= 3  # 54 240 B (two resident) before the model
+    if p == 100:
+        # the reference horizon: the delayed inputs' lines are rings of D + m
+        # entries and the C_hat rows overlay the hand-off areas, so two
+        # four-wave workgroups share a CU (ser-coop was 107 584 B, one per CU)
+        assert 160 * 1024 // alloc >= 2
 
 
 def test_rows_lds_model_python_mirror_agrees():

@@ -34,7 +34,11 @@ def layout(d, over=None):
         o += over.get("pad_%d" % c, 0)
         lo[c] = o
         D = d["delay"][c]
-        o += ES * ((U + 1) if D == 0 else (M - 1) + max(0, p - D))
+        n = (U + 1) if D == 0 else (M - 1) + max(0, p - D)
+        # (rows_layout.cpp rings a delayed line at D + m entries when p > 2 D + 1;
+        # this mirror covers plain lines only, as at the bench configuration)
+        assert D == 0 or n <= D + M, "ring lines are not modelled here"
+        o += ES * n
     L["lo"] = lo
     o += over.get("pad_dump", 0)
     L["dump_off"] = o
@@ -46,10 +50,11 @@ def layout(d, over=None):
     L["zr_off"] = o
     o += U * ES
     L["LQ"] = up(o, 2) + over.get("pad_LQ", 0)
-    # wave region [lines 4 x LQ][C_hat 4 x ny x 16][w tables 4 x nd x WL], at
-    # least the four staged records (rows_layout.cpp make_layout)
-    L["ch_off"] = 4 * L["LQ"]
-    L["w_off"] = L["ch_off"] + 4 * ny * 16 + over.get("pad_w", 0)
+    # wave region [lines 4 x LQ, C_hat 4 x ny x 16 overlaid][w tables 4 x nd x WL],
+    # at least the four staged records (rows_layout.cpp make_layout)
+    chs = 4 * ny * 16
+    L["ch_off"] = 0 if 4 * L["LQ"] >= chs else 4 * L["LQ"]
+    L["w_off"] = max(4 * L["LQ"], L["ch_off"] + chs) + over.get("pad_w", 0)
     # w lines end at D + 3 entries (the carriers read the zero slots from r = D)
     L["WL"] = up(min(p + 2 + U, max(d["delay"]) + 3), 2) + over.get("pad_WL", 0)
     L["per_wave"] = max(up(L["w_off"] + 4 * d["nd"] * L["WL"], 2), up(4 * d["rec_len"], 2)) + over.get("pad_wave", 0)
