@@ -93,7 +93,10 @@
 #ifndef CMPC_ROWS_WPE
 #define CMPC_ROWS_WPE 3  // waves per SIMD the kernel is compiled and launched for
 #endif
-template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG>
+// RING: some delayed input's hand-off line is a ring (RowsLayout::ring; p > 2 D + 1):
+// the wrap bookkeeping and the longer segment list only where needed, so the
+// bench kernel (p = 50) keeps its registers (167 VGPRs, no scratch).
+template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG, bool RING>
 __global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(CMPC_ROWS_WPE, CMPC_ROWS_WPE)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -168,7 +171,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
   for (int k = 0; k < NDW; ++k)
     if (cl && k == kc && dlen[k] < pp) ysw = dlen[k];
   const int nseg = P.rows.nseg;
-  constexpr int NSEG = 5 * NDW;  // segment bounds come from the delayed inputs (D, p - D, ring wraps)
+  // segment bounds: the delayed inputs' D and p - D (and the ring wraps)
+  constexpr int NSEG = RING ? CMPC_ROWS_NSEG : 2 * NDW;
   int segb[NSEG];
 #pragma unroll
   for (int i = 0; i < NSEG; ++i) segb[i] = P.rows.seg[i];
@@ -194,15 +198,15 @@ void cmpc_build_rows_kernel(BuildParams P) {
   // ring lines (RowsLayout::ring): the writer and each gather reader step back
   // by the ring at their wrap steps (rows_layout.cpp, rows_ring_*_wrap)
   int ringw = 0, ringr = 0;
+  if constexpr (RING) {
 #pragma unroll
-  for (int c = 0; c < NUT; ++c) {
-    if (c == cm) ringw = P.rows.ring[c];
-    if (c == gc) ringr = P.rows.ring[c];
+    for (int c = 0; c < NUT; ++c) {
+      if (c == cm) ringw = P.rows.ring[c];
+      if (c == gc) ringr = P.rows.ring[c];
+    }
   }
-  const int wwr = (wdel && ringw) ? ringw - (M - 1) : -1;
-  const int wback = ringw * NY;
-  const int rwr = (rdel && ringr) ? ringr + dg - (M - 1 - gk) : -1;
-  const int rback = ringr * NY;
+  const int wwr0 = (wdel && ringw) ? ringw - (M - 1) : -1;  // first wraps; then every ring steps
+  const int rwr0 = (rdel && ringr) ? ringr + dg - (M - 1 - gk) : -1;
   const bool tl = M > 1 && mk && dm == 0;  // ring writer: copies each group's last value to entry -1
   double* const tq = qlines + lom;
   // every lane stores each step (no exec-mask branches in the loop): lanes
@@ -394,6 +398,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     double* wq = w_start;
     double* rq = r_start;
     int winc = winc0, rinc = 0;
+    int wwr = wwr0, rwr = rwr0;
 
     // Optional L2 prefetch of this wave's next group of records (one dword
     // per 128-byte line, consumed after the horizon loop).  Off: since the
@@ -491,9 +496,11 @@ void cmpc_build_rows_kernel(BuildParams P) {
         yp += yinc;
       }
       if (r == rsw) { rq = r_line; rinc = NY; }
-      if (r == rwr) rq -= rback;
-      if (r == wwr) wq -= wback;
-      if (r == wsw) { wq = dump; winc = 0; }
+      if constexpr (RING) {
+        if (r == rwr) { rq -= ringr * NY; rwr += ringr; }
+        if (r == wwr) { wq -= ringw * NY; wwr += ringw; }
+      }
+      if (r == wsw) { wq = dump; winc = 0; wwr = -1; }
       if (r == ysw) { yp = zeros; yinc = 0; }
     }
 #undef CMPC_ROWS_STEP
@@ -550,9 +557,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // ---------------------------------------------------------------------------
 // Waves per workgroup (4, or 2 where that holds 1.5x the resident waves;
 // cmpc_rows_waves_per_group in rows_layout.cpp).
-template <int NS, int NY, int NU, int M, int WPG>
+template <int NS, int NY, int NU, int M, int WPG, bool RING>
 static int rows_launch(const BuildParams& P, hipStream_t s) {
-  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG>;
+  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG, RING>;
   const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * WPG);
   if (lds > 160 * 1024) return -1;
   if (lds > 64 * 1024)
@@ -574,16 +581,23 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
 
 #define ROWS_CASE(NS_, NY_, NU_, M_)                                                  \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
-    switch (cmpc_rows_waves_per_group(P.rows)) {                                      \
-      case 4: return rows_launch<NS_, NY_, NU_, M_, 4>(P, s);                         \
-      case 2: return rows_launch<NS_, NY_, NU_, M_, 2>(P, s);                         \
-      default: return -1;                                                             \
-    }                                                                                 \
+    const int w_ = cmpc_rows_waves_per_group(P.rows);                                  \
+    if (ring) {                                                                        \
+      if (w_ == 4) return rows_launch<NS_, NY_, NU_, M_, 4, true>(P, s);               \
+      if (w_ == 2) return rows_launch<NS_, NY_, NU_, M_, 2, true>(P, s);               \
+    } else {                                                                           \
+      if (w_ == 4) return rows_launch<NS_, NY_, NU_, M_, 4, false>(P, s);              \
+      if (w_ == 2) return rows_launch<NS_, NY_, NU_, M_, 2, false>(P, s);              \
+    }                                                                                  \
+    return -1;                                                                         \
   }
 
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!P.rows.ok) return -1;
+  bool ring = false;
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) ring = ring || P.rows.ring[c] > 0;
+  if (!ring && P.rows.nseg > 2 * 2) return -1;  // the plain kernel unrolls over 2 ND bounds
   ROWS_CASE(11, 3, 2, 2)  // parallel coop        (ControlledOutputIndices <0,1,3>)
   ROWS_CASE(11, 2, 2, 2)  // parallel ncoop
   ROWS_CASE(11, 3, 4, 2)  // parallel centralized

@@ -28,6 +28,7 @@ inline void cmpc_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t
 #ifndef CMPC_ROWS_U
 #define CMPC_ROWS_U 4            // horizon unroll of the row build kernel (4 or 5; 5 measured no faster)
 #endif
+#define CMPC_ROWS_NSEG 16        // loop segment bounds of the row build kernel
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 #define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
 
@@ -49,8 +50,8 @@ struct CfgOffsets {
 // entries and a zero area (U entries each).
 // A delayed input's line is a ring of D + m entries when its p - D values
 // would need more (p > 2 D + 1): the writer and the two gather readers step
-// back by ring[c] entries at their wrap steps, which are loop segment bounds
-// too.  The C_hat rows overlay the hand-off areas: they are read in the
+// back by ring[c] entries at each of their wrap steps (every ring[c] steps),
+// which are loop segment bounds too (at most CMPC_ROWS_NSEG of them).  The C_hat rows overlay the hand-off areas: they are read in the
 // prologue only, before the zero areas are written.
 struct RowsLayout {
   int ok;                        // the row kernel can run these dimensions
@@ -59,7 +60,7 @@ struct RowsLayout {
   int LQ, lo[CMPC_MAX_INPUTS], dump_off, z_off, zr_off;
   int ring[CMPC_MAX_INPUTS];      // entries of a wrapping delayed line, 0: a plain line
   int ch_off, w_off, WL;
-  int nseg, seg[5 * CMPC_MAX_INPUTS];  // ascending distinct D, p - D and wrap steps inside (0, p)
+  int nseg, seg[CMPC_ROWS_NSEG];  // ascending distinct D, p - D and wrap steps inside (0, p)
 };
 
 struct BuildParams {

@@ -98,22 +98,29 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
   // loop segments: distinct D (delayed readers start) and p - D (delayed
   // writers stop) inside (0, p), ascending
   R->nseg = 0;
+  bool fits = true;
   auto add = [&](int v) {
     if (v <= 0 || v >= d.p) return;
     for (int i = 0; i < R->nseg; ++i)
       if (R->seg[i] == v) return;
+    if (R->nseg == CMPC_ROWS_NSEG) {
+      fits = false;
+      return;
+    }
     R->seg[R->nseg++] = v;
   };
   for (int c = 0; c < d.nu_tot; ++c)
     if (d.delay[c] > 0) {
       add(d.delay[c]);
       add(d.p - d.delay[c]);
-      if (R->ring[c]) {  // wrap steps: the writer's, and each move's gather reader's
-        add(rows_ring_writer_wrap(R->ring[c], M));
-        for (int k = 0; k < M; ++k) add(rows_ring_reader_wrap(R->ring[c], d.delay[c], M, k));
+      if (R->ring[c]) {  // wrap steps: the writer's (while it writes), each move's gather reader's
+        for (int t = rows_ring_writer_wrap(R->ring[c], M); t < d.p - d.delay[c]; t += R->ring[c]) add(t);
+        for (int k = 0; k < M; ++k)
+          for (int t = rows_ring_reader_wrap(R->ring[c], d.delay[c], M, k); t < d.p; t += R->ring[c]) add(t);
       }
     }
   std::sort(R->seg, R->seg + R->nseg);
+  if (!fits) R->nseg = -1;  // too many segments: not usable (make_layout's caller checks)
   return sizeof(double) * ((size_t)R->lds_block + (size_t)R->per_wave * CMPC_BUILD_WAVES);
 }
 
@@ -251,9 +258,9 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     }
     for (int l = 0; l < 64; ++l) {
       if (r == rsw[l]) { rq[l] = rline[l]; rinc[l] = NY; }
-      if (r == rwr[l]) rq[l] -= rback[l];
-      if (r == wwr[l]) wq[l] -= wback[l];
-      if (r == wsw[l]) { wq[l] = dump[l]; winc[l] = 0; }
+      if (r == rwr[l]) { rq[l] -= rback[l]; rwr[l] += rback[l] / NY; }
+      if (r == wwr[l]) { wq[l] -= wback[l]; wwr[l] += wback[l] / NY; }
+      if (r == wsw[l]) { wq[l] = dump[l]; winc[l] = 0; wwr[l] = -1; }
       if (r == ysw[l]) { yp[l] = 0; yinc[l] = 0; }  // the zero slots
     }
   }
@@ -328,6 +335,13 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
   RowsLayout best;
   make_layout(d, nd, rec_len, base, &best);
+  if (best.nseg < 0) {  // more loop segments than the kernel unrolls over: not usable
+    best.ok = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    cache[key] = best;
+    *out = best;
+    return;
+  }
   const int base_waves = resident_waves(best);
   // CMPC_ROWS_LAYOUT=packed: regions back to back (diagnostic A/B timing)
   const char* env = std::getenv("CMPC_ROWS_LAYOUT");

@@ -141,3 +141,19 @@ def test_rows_lds_model_python_mirror_agrees():
     d = dict(sim.PAR_COOP, p=50)
     L = sim.layout(d)
     assert abs(sim.simulate(d, L, 0)[1] - packed) < 1e-9
+
+
+@pytest.mark.parametrize("p", [20, 50, 81, 82, 83, 100, 163, 200, 250])
+def test_row_kernel_ring_protocol(p):
+    """The row kernel's delayed-input hand-off (lines, or rings of D + m
+    entries with the writer and readers stepping back at every wrap), emulated
+    with the kernel's segment bounds and unrolled blocks: every gather read at
+    step s returns h_{s-k-D} (zero before the line starts), no access leaves
+    the line, and the library's layout agrees on when a ring is used."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ring_protocol_check as rp
+    errs, ring, nseg = rp.check(p, 40)
+    assert errs == 0
+    assert (ring > 0) == (p > 2 * 40 + 1)
+    assert nseg <= 16

@@ -68,9 +68,12 @@ def oracle_qps(cfg, arr, lin, u_old):
     return np.stack(Hs), np.stack(fs), np.stack(Gs)
 
 
+# p = 100 and 200 run the row kernel's ring lines (one wrap at p = 100, three
+# per line at p = 200: rows_layout.cpp)
 BUILD_CASES = [("par", "coop", 20), ("par", "coop", 50), ("par", "ncoop", 50),
                ("par", "cent", 50), ("par", "coop", 100), ("ser", "ncoop", 50),
-               ("ser", "coop", 50), ("ser", "cent", 50), ("ser", "coop", 100)]
+               ("ser", "coop", 50), ("ser", "cent", 50), ("ser", "coop", 100),
+               ("ser", "cent", 100), ("par", "cent", 200)]
 
 
 def setup_for(plant, ctype):
