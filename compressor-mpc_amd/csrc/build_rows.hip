@@ -93,6 +93,7 @@
 #ifndef CMPC_ROWS_WPE
 #define CMPC_ROWS_WPE 3  // waves per SIMD the kernel is compiled and launched for
 #endif
+
 // RING: some delayed input's hand-off line is a ring (RowsLayout::ring; p > 2 D + 1):
 // the wrap bookkeeping and the longer segment list only where needed, so the
 // bench kernel (p = 50) keeps its registers (167 VGPRs, no scratch).

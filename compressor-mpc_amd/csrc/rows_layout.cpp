@@ -37,6 +37,7 @@ struct Pads {
   int order[CMPC_MAX_INPUTS];
   int pad_c[CMPC_MAX_INPUTS];
   int dump, z, zr, LQ, yl, yls, w, WL;
+  int ring;  // ring lines where p > 2 D + 1 (only when that keeps more waves resident)
 };
 
 int up(int v, int a) { return (v + a - 1) / a * a; }
@@ -62,7 +63,7 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
     int len = (d.delay[c] == 0) ? U + 1 : (M - 1) + std::max(0, d.p - d.delay[c]);
     // a value written at step t is read until step t + D + m - 1: a ring of
     // D + m entries holds every value still to be read (rows_ring_* below)
-    if (d.delay[c] > 0 && len > d.delay[c] + M) {
+    if (pd.ring && d.delay[c] > 0 && len > d.delay[c] + M) {
       len = d.delay[c] + M;
       R->ring[c] = len;
     }
@@ -335,6 +336,20 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
   RowsLayout best;
   make_layout(d, nd, rec_len, base, &best);
+  {
+    // ring lines (and the kernel's RING instantiation, whose wrap bookkeeping
+    // costs registers) only where they let more waves share a CU: ser-coop /
+    // ser-cent p = 100 go from one four-wave workgroup per CU to two, while
+    // par-coop p = 100 has two either way and keeps its plain lines
+    Pads rb = base;
+    rb.ring = 1;
+    RowsLayout rl;
+    make_layout(d, nd, rec_len, rb, &rl);
+    if (rl.nseg >= 0 && (best.nseg < 0 || resident_waves(rl) > resident_waves(best))) {
+      base = rb;
+      best = rl;
+    }
+  }
   if (best.nseg < 0) {  // more loop segments than the kernel unrolls over: not usable
     best.ok = 0;
     std::lock_guard<std::mutex> lk(mu);
@@ -402,6 +417,7 @@ extern "C" int cmpc_rows_lds_model(const cmpc_dims* d, double* packed_cycles, do
   if (!R.ok) return -1;
   Pads base{};
   for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.order[c] = c;
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) base.ring = base.ring || R.ring[c] > 0;
   RowsLayout P0;
   make_layout(*d, L.nd, L.rec_len, base, &P0);
   if (packed_cycles) *packed_cycles = loop_conflicts(*d, L.nd, P0, 0);
