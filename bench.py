@@ -541,8 +541,10 @@ def main():
         coupled.update({
             "qp_solves_per_s": world * rc["qp_per_gpu"] * K * rc["steps"] / el_c,
             "ms_per_step": el_c / rc["steps"] * 1e3,
-            "exchange": ("RCCL all_gather_into_tensor of B x S_local x nV plans per Jacobi iteration "
-                         f"({args.dist_backend})" if world > 1 else "local copy (world size 1)"),
+            "exchange": ("RCCL all_gather_into_tensor of B x S_local x nV plans per Jacobi iteration"
+                         if world > 1 and args.dist_backend == "nccl" else
+                         "gloo all_gather of the plans through host memory (rehearsal only)" if world > 1
+                         else "local copy (world size 1)"),
             "note": "SURVEY config 4: S_total = 8 x world sub-controllers per scenario (synthetic "
                     "coupling, cmpc/coupled.py), 8 per GPU; step = build + K x (all-gather + "
                     "coupled iteration), first move applied; per-GPU work grows with S_total "

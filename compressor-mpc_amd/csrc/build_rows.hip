@@ -243,7 +243,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     const int q = 4 * g + R;
     const bool qv = q < nqp;
     const int qq = qv ? q : nqp - 1;
-    const int s = qq % S;
+    const int s = qq & (S - 1);  // S divides 64 (cmpc_create), a power of two
     const double* lwt = lw_all + s * NY * NY;
     double* chq = chs + R * NY * 16;
 
