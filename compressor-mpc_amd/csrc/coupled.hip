@@ -58,14 +58,21 @@ void cmpc_coupled_kernel(CoupledParams P) {
   for (int i = 0; i < N; ++i) hmax = fabs(H[i][i]) > hmax ? fabs(H[i][i]) : hmax;
   const double tol_d = TOL_D * (1.0 + hmax);
 
-  // f_k = f + G_ext du_other (other sub-controllers in global order)
+  // f_k = f + G_ext du_other (other sub-controllers in global order).  The
+  // loop runs over G_ext's column blocks jj (the same for every lane, so each
+  // element read is one contiguous row segment of the wave's QPs) and maps
+  // jj to the other controller j (skipping this one); four blocks per trip
+  // keep 64 G_ext loads per lane in flight.  The sum order (j, then a, then
+  // v) is unchanged.
   const int nvo = (P.S_total - 1) * N;
   double fk[N];
 #pragma unroll
   for (int a = 0; a < N; ++a) fk[a] = f[a];
-  for (int j = 0; j < P.S_total; ++j) {
-    if (j == sg) continue;
-    const int jj = j < sg ? j : j - 1;
+  const size_t rs = (size_t)N * P.nqp;  // stride of one column block (N rows of G_ext)
+  const double* gq = P.G_ext + q;
+#pragma unroll 4
+  for (int jj = 0; jj < P.S_total - 1; ++jj) {
+    const int j = jj < sg ? jj : jj + 1;
     const int rj = j / P.S_local, slj = j - rj * P.S_local;
     const double* dj = P.du_all + (((size_t)rj * P.B + b) * P.S_local + slj) * N;
     double d[N];
@@ -75,7 +82,7 @@ void cmpc_coupled_kernel(CoupledParams P) {
     for (int a = 0; a < N; ++a)
 #pragma unroll
       for (int v = 0; v < N; ++v)
-        fk[a] = fk[a] + P.G_ext[((size_t)a * nvo + jj * N + v) * P.nqp + q] * d[v];
+        fk[a] = fk[a] + gq[(size_t)a * nvo * P.nqp + jj * rs + (size_t)v * P.nqp] * d[v];
   }
 
   double x[N];
