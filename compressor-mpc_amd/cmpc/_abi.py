@@ -114,6 +114,14 @@ def load_library(path: str = LIB_PATH):
         raise RuntimeError(
             f"{path} not found: build it with `make -C compressor-mpc_amd/csrc` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same
+    # soname).  Loaded first, it also serves this library; loaded after ours,
+    # torch brings in a second runtime that finds no GPU ("No HIP GPUs are
+    # available") and whose device pointers and streams ours cannot use.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P = ctypes.POINTER
     c_void = ctypes.c_void_p

@@ -489,6 +489,18 @@ void cmpc_build_rows_kernel(BuildParams P) {
         rq += U * rinc;
         yp += U * yinc;
       }
+      // a remainder of two or three steps starts with a two-step block: its
+      // chain registers alternate as in the unrolled loop (a one-step loop
+      // copies them back, 11 moves a step)
+      if (U > 2 && r + 2 <= r_end) {
+        CMPC_ROWS_STEP(0)
+        CMPC_ROWS_STEP(1)
+        CMPC_ROWS_TAIL()
+        wq += 2 * winc;
+        rq += 2 * rinc;
+        yp += 2 * yinc;
+        r += 2;
+      }
       for (; r < r_end; ++r) {
         CMPC_ROWS_STEP(0)
         CMPC_ROWS_TAIL()

@@ -252,6 +252,13 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
       tail();
       advance(U);
     }
+    if (U > 2 && r + 2 <= r_end) {  // the kernel's two-step remainder block
+      step(0);
+      step(1);
+      tail();
+      advance(2);
+      r += 2;
+    }
     for (; r < r_end; ++r) {
       step(0);
       tail();

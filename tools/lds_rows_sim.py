@@ -203,6 +203,13 @@ def simulate(d, L, wave=0, verbose=False):
             for ln in lanes:
                 ln["wq"] += U * ln["winc"]; ln["rq"] += U * ln["rinc"]; ln["yp"] += U * ln["yinc"]
             r += U
+        if U > 2 and r + 2 <= r_end:  # the kernel's two-step remainder block
+            step(0)
+            step(1)
+            tail()
+            for ln in lanes:
+                ln["wq"] += 2 * ln["winc"]; ln["rq"] += 2 * ln["rinc"]; ln["yp"] += 2 * ln["yinc"]
+            r += 2
         while r < r_end:
             step(0)
             tail()

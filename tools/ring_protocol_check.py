@@ -74,6 +74,15 @@ def check(p, D, M=2, U=4):
                 if rq[k] is not None:
                     rq[k] += U * rinc[k]
             r += U
+        if U > 2 and r + 2 <= r_end:  # the two-step remainder block
+            step(0)
+            step(1)
+            if wq is not None:
+                wq += 2 * winc
+            for k in range(M):
+                if rq[k] is not None:
+                    rq[k] += 2 * rinc[k]
+            r += 2
         while r < r_end:
             step(0)
             if wq is not None:
