@@ -187,7 +187,7 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     rback[lane] = rgr * NY;
     tl[lane] = M > 1 && mk[lane] && dm == 0;
     tq[lane] = ql + R.lo[cm];
-    zq[lane] = ql + R.z_off + oo;
+    zq[lane] = ol[lane] ? ql + R.z_off + oo : dump[lane];  // every lane stores (build_rows.hip)
     if (st) {
       yp[lane] = 0; yinc[lane] = 0;
     } else if (ol[lane]) {
@@ -214,10 +214,10 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
     read_b64(a);
     for (int o = 0; o < NY; ++o) {
       for (int l = 0; l < 64; ++l) a[l] = wq[l] + u * NY + o;
-      by16(a, mk);
+      by16(a, all);  // lanes without a Markov role store into the dump area
     }
     for (int l = 0; l < 64; ++l) a[l] = zq[l] + u * NY;
-    by16(a, ol);
+    by16(a, all);
     for (int o = 0; o < NY;) {
       for (int l = 0; l < 64; ++l) a[l] = rq[l] + u * NY + o;
       if (o + 1 < NY) {  // the compiler pairs the reads into ds_read2_b64

@@ -10,10 +10,15 @@ Replays the kernel's per-lane pointer arithmetic step by step for one wave
 and prints the extra (conflict) cycles per wave-step of each instruction.
 usage: python tools/lds_rows_sim.py [p] [layout json overrides]"""
 import json
+import os
+import re
 import sys
 from collections import defaultdict
 
-U = 4
+# the kernel's horizon unroll (CMPC_ROWS_U, cmpc_internal.h)
+U = int(re.search(r"#define CMPC_ROWS_U (\d+)", open(os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "..", "compressor-mpc_amd", "csrc",
+    "cmpc_internal.h")).read()).group(1))
 
 
 def up(v, a):
