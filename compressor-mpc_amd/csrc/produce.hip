@@ -38,17 +38,22 @@ constexpr int kMat = 121;          // ns x ns, ns <= 11
 // registers before the first store, and one wave's LDS operations complete
 // in order.  (Separate arrays: 2 waves/SIMD by LDS, 0.140 ms at 65 536
 // scenarios; aliased, with the table sized by S: 4 waves/SIMD.)
-constexpr int kScnLds = kMat + 2 * 44 + 11 + 2 * 11 + 3 + 4;
+constexpr int kScnLds = kMat + 2 * 44 + 11 + 2 * 11 + 3 + 4 + 2;
+// the last two entries of a scenario's region hold 0.0 and 1.0, so that every
+// record element before the observer tail is one table-indexed LDS read
+constexpr int kZeroSlot = kScnLds - 2, kOneSlot = kScnLds - 1;
 
 // Source of record element e of sub-controller s (same for every scenario):
-// >= 0: offset in the scenario's LDS region (Ad, Bd, Cc, fd); kZero, kOne;
-// kDx + i: observer tail element i; kY + o: plant output o.
-constexpr int kZero = -1, kOne = -2, kDx = -1000, kY = -100;
+// >= 0: offset in the scenario's LDS region (Ad, Bd, Cc, fd, or the 0.0 and
+// 1.0 slots); kDx + i: observer tail element i; kY + o: plant output o;
+// kZero: padding after y.
+constexpr int kZero = -1, kDx = -1000, kY = -100;
 
 template <int PLANT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams P) {
   __shared__ double lds[kWaves * kSpw * kScnLds];
-  extern __shared__ int src[];  // S x rec_len (dynamic, cmpc_launch_produce)
+  extern __shared__ int src[];  // S x rec_len, then naug (dynamic, cmpc_launch_produce)
+  int* dmap = src + P.S * P.rec_len;  // observer tail entry -> its position in the dx row
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane / kLanes, l = lane - g * kLanes;  // scenario row, lane in row
   // unit: scenario b (S records), or in per-QP mode QP slot q (its record)
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   // element -> source table (built once per workgroup)
   for (int t = threadIdx.x; t < P.S * P.rec_len; t += 64 * kWaves) {
     const int s = t / P.rec_len, e = t - s * P.rec_len;
-    int v = kZero;
+    int v = e < P.off_x ? kZeroSlot : kZero;
     const int oAd = (int)(Ad - w), oBd = (int)(Bd - w), oCc = (int)(Cc - w), ofd = (int)(fd - w);
     if (e >= P.off_A && e < P.off_A + ns * ns) {
       v = oAd + (e - P.off_A);
@@ -76,7 +81,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
     } else if (e >= P.off_C && e < P.off_C + P.ny * P.nobs) {
       const int o = (e - P.off_C) / P.nobs, k = e - P.off_C - o * P.nobs;
       const int oi = P.out_idx[s][o];
-      v = (k < ns) ? oCc + oi * ns + k : ((oi == k - ns) ? kOne : kZero);
+      v = (k < ns) ? oCc + oi * ns + k : ((oi == k - ns) ? kOneSlot : kZeroSlot);
     } else if (e >= P.off_f && e < P.off_f + ns) {
       v = ofd + (e - P.off_f);
     } else if (e >= P.off_x && e < P.off_x + P.naug) {
@@ -85,6 +90,22 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
       v = kY - P.out_idx[s][e - P.off_y];
     }
     src[t] = v;
+  }
+  // logical entry e of a ring-stored delay block (observer state,
+  // cmpc_obs_prior_kernel) -> its position in the row; the same for every unit
+  for (int e = threadIdx.x; e < P.naug; e += 64 * kWaves) {
+    int pe = e;
+    for (int k = 0; k < P.nring; ++k)
+      if (e >= P.rb[k] && e < P.rb[k] + P.rlen[k]) {
+        const int i = e - P.rb[k] + P.rot[k];
+        pe = P.rb[k] + (i >= P.rlen[k] ? i - P.rlen[k] : i);
+      }
+    dmap[e] = pe;
+  }
+  if ((threadIdx.x & (kLanes - 1)) == 0) {
+    double* wz = lds + (threadIdx.x / kLanes) * kScnLds;
+    wz[kZeroSlot] = 0.0;
+    wz[kOneSlot] = 1.0;
   }
   __syncthreads();
 
@@ -137,16 +158,18 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
       prop1_dpp<ns>(a2[i], ycol, z);
       a3[i] = z;
     }
-    // Ac (element-wise, lane j holds column j) and Ac [A | B | f]
+    // Ac (element-wise, lane j holds column j) and Ac [A | B | f]; lane j
+    // stores row i of its column at a per-lane base and stride (Ad, Bd or fd)
+    double* const dst = (l < ns) ? Ad + l : (l < ns + 4) ? Bd + (l - ns) : fd;
+    const int dstride = (l < ns) ? ns : (l < ns + 4) ? 4 : 1;
+    const bool dstore = l < ns + 5;
 #pragma unroll
     for (int i = 0; i < ns; ++i) {
       const double ac = Ts * (i == l) + Ts * Ts / 2.0 * ycol[i] + Ts * Ts * Ts / 6.0 * a2[i] +
                         Ts * Ts * Ts * Ts / 24.0 * a3[i];
       double z = 0.0;
       prop1_dpp<ns>(ac, ycol, z);
-      if (l < ns) Ad[i * ns + l] = z + (i == l ? 1.0 : 0.0);
-      else if (l < ns + 4) Bd[i * 4 + (l - ns)] = z;
-      else if (l == ns + 4) fd[i] = z;
+      if (dstore) dst[i * dstride] = (i == l) ? z + 1.0 : z;
     }
     WAVE_SYNC();
   }
@@ -176,8 +199,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + u * kLanes;
-        const int t = e < P.off_x ? srow[e] : kZero;
-        v[u] = (t >= 0) ? w[t] : (t == kOne ? 1.0 : 0.0);
+        v[u] = w[e < P.off_x ? srow[e] : kZeroSlot];
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)
@@ -189,16 +211,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + u * kLanes;
-        // logical entry e of a ring-stored delay block (observer state,
-        // cmpc_obs_prior_kernel) -> its position in the row
-        int pe = e;
-#pragma unroll
-        for (int k = 0; k < CMPC_ND_MAX; ++k)
-          if (k < P.nring && e >= P.rb[k] && e < P.rb[k] + P.rlen[k]) {
-            const int i = e - P.rb[k] + P.rot[k];
-            pe = P.rb[k] + (i >= P.rlen[k] ? i - P.rlen[k] : i);
-          }
-        v[u] = (dx && e < P.naug) ? dx[pe] : 0.0;
+        v[u] = (dx && e < P.naug) ? dx[dmap[e]] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)
@@ -218,7 +231,7 @@ int cmpc_launch_produce(const ProduceParams& P, int plant, void* stream) {
   const int units = P.per_qp ? P.B * P.S : P.B;
   const int grid = (units + kWaves * kSpw - 1) / (kWaves * kSpw);
   if (P.S < 1 || P.S > CMPC_MAX_S_PRODUCE || P.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return -1;
-  const size_t table = sizeof(int) * (size_t)P.S * P.rec_len;
+  const size_t table = sizeof(int) * ((size_t)P.S * P.rec_len + (size_t)P.naug);
   if (plant == CMPC_PLANT_PARALLEL)
     cmpc_launch(cmpc_produce_kernel<CMPC_PLANT_PARALLEL>, dim3(grid), dim3(64 * kWaves), table, s, P);
   else if (plant == CMPC_PLANT_SERIAL)
