@@ -227,6 +227,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for the barrier and the max over ranks "
                          "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="set up the process group and run the collectives even at world size 1 "
+                         "(an RCCL communicator of one rank: exercises the multi-GPU code path "
+                         "on a one-GPU box)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -240,7 +244,7 @@ def main():
         local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -530,7 +534,8 @@ def main():
     if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench
         rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
-                               steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds)
+                               steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds,
+                               force_collective=bool(dist))
         tc = torch.tensor([rc["elapsed_s"]], dtype=torch.float64,
                           device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
         if dist:
@@ -542,8 +547,8 @@ def main():
             "qp_solves_per_s": world * rc["qp_per_gpu"] * K * rc["steps"] / el_c,
             "ms_per_step": el_c / rc["steps"] * 1e3,
             "exchange": ("RCCL all_gather_into_tensor of B x S_local x nV plans per Jacobi iteration"
-                         if world > 1 and args.dist_backend == "nccl" else
-                         "gloo all_gather of the plans through host memory (rehearsal only)" if world > 1
+                         if dist and args.dist_backend == "nccl" else
+                         "gloo all_gather of the plans through host memory (rehearsal only)" if dist
                          else "local copy (world size 1)"),
             "note": "SURVEY config 4: S_total = 8 x world sub-controllers per scenario (synthetic "
                     "coupling, cmpc/coupled.py), 8 per GPU; step = build + K x (all-gather + "

@@ -75,11 +75,15 @@ class CoupledRank:
     rank's B scenarios x S_local sub-controllers (coop dims, S = 2 setup),
     G_ext, the local and gathered plan buffers, and the RCCL all-gather."""
 
-    def __init__(self, ctx, S_total: int, S_local: int, rank: int, world: int, G_ext, group=None):
+    def __init__(self, ctx, S_total: int, S_local: int, rank: int, world: int, G_ext, group=None,
+                 force_collective: bool = False):
         import torch
         self.torch = torch
         self.ctx, self.S_total, self.S_local = ctx, S_total, S_local
         self.rank, self.world, self.group = rank, world, group
+        # world size 1 copies the plans locally unless told to run the
+        # collective (a one-rank RCCL communicator: the multi-GPU code path)
+        self.force_collective = force_collective
         self.s_offset = rank * S_local
         nqp = ctx.B * ctx.cfg.S
         if nqp % S_local:
@@ -95,7 +99,7 @@ class CoupledRank:
 
     def gather(self):
         import torch.distributed as dist
-        if self.world == 1:
+        if self.world == 1 and not self.force_collective:
             self.du_all[0].copy_(self.du_local)
             return
         if dist.get_backend(self.group) == "nccl":
@@ -125,7 +129,7 @@ class CoupledRank:
 
 def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: int = 4096, p: int = 50,
                       K: int = 9, steps: int = 20, warmup: int = 3, settle_seconds: float = 0.25,
-                      S_total: int = 0, group=None) -> dict:
+                      S_total: int = 0, group=None, force_collective: bool = False) -> dict:
     """SURVEY config 4 on this rank: B scenarios x S_local sub-controllers
     (global indices rank * S_local + i of S_total = S_local * world), one
     step = build + K x (all-gather of the plans, coupled Jacobi iteration),
@@ -156,7 +160,8 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
         ctx.init_warmstart()
         _, _, G = ctx.download_qp()
         G_ext = torch.from_numpy(synthetic_g_ext(G, S_total, S_local, rank * S_local)).to(f"cuda:{device}")
-        cr = CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group)
+        cr = CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group,
+                         force_collective=force_collective)
         for _ in range(warmup):
             cr.step(K)
         torch.cuda.synchronize(device)
@@ -164,7 +169,7 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
         while time.perf_counter() < t_end:
             cr.step(K)
             torch.cuda.synchronize(device)
-        if world > 1:
+        if world > 1 or force_collective:
             dist.barrier(group=group)
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()

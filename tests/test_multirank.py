@@ -157,3 +157,99 @@ def test_gpu_two_ranks_match_single_process():
     assert np.array_equal(d_all, d_ref)
     assert np.array_equal(st_all, st_ref)
     assert np.array_equal(u_all, u_ref)
+
+
+def _rccl_worker(port, q):
+    """One rank with a real RCCL (nccl) communicator of world size 1."""
+    import torch
+    import torch.distributed as dist
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.coupled import CoupledRank, synthetic_g_ext
+    from cmpc.sharding import gather_to_all
+    from cmpc.synthetic import synthetic_batch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        # scenario sharding's result gather on the device
+        a = np.arange(2 * 37 * 3, dtype=np.float64).reshape(2 * 37, 3)
+        g_ok = bool(np.array_equal(gather_to_all(a, 2 * 37, 2), a))
+        # config 4's plan all-gather (all_gather_into_tensor) against the local copy
+        cfg = cmpc.reference_config("par", "coop", p=20)
+        arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+        S_local, B, K = 8, 64, 9
+        nqp = B * S_local
+        lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=77, n_distinct=64)
+        plans = []
+        for force in (False, True):
+            ctx = cmpc.Context(cfg, nqp // cfg.S, device=0)
+            try:
+                ctx.configure(arr)
+                ctx.set_state(u_old, np.zeros((nqp, cfg.nV)), np.zeros(nqp, np.uint32))
+                ctx.upload_lin(lin)
+                ctx.build()
+                ctx.init_warmstart()
+                _, _, G = ctx.download_qp()
+                G_ext = torch.from_numpy(synthetic_g_ext(G, S_local, S_local, 0)).cuda()
+                cr = CoupledRank(ctx, S_local, S_local, 0, 1, G_ext, force_collective=force)
+                for _ in range(2):
+                    cr.step(K)
+                torch.cuda.synchronize()
+                du, st, _ = ctx.download()
+                plans.append((du, st))
+            finally:
+                ctx.close()
+        c_ok = bool(np.array_equal(plans[0][0], plans[1][0]) and np.array_equal(plans[0][1], plans[1][1]))
+        # the bench's timing reductions
+        t = torch.tensor([1.5], dtype=torch.float64, device="cuda:0")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        q.put((g_ok, c_ok, float(t.item()), int((plans[1][1] == 0).sum()), nqp))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_single_rank_paths():
+    """The multi-GPU code paths on a one-GPU box: an RCCL (nccl) process group
+    of one rank runs the device gather of the scenario shards, config 4's plan
+    all_gather_into_tensor (equal bit for bit to the local copy it replaces)
+    and the bench's barrier and max reduction.  (RCCL refuses two ranks on one
+    device; the 8-GPU run is the driver's.)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    g_ok, c_ok, tmax, n_ok, nqp = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert g_ok and c_ok
+    assert tmax == 1.5
+    assert n_ok == nqp
+
+
+@pytest.mark.gpu
+def test_gpu_bench_force_dist_single_rank():
+    """bench.py under torch.distributed.run with one rank and --force-dist:
+    the RCCL process group, barrier, max over ranks and the coupled section's
+    all-gather run as in the driver's N-GPU launch, and the line reports the
+    RCCL exchange."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "1", "--force-dist", "--steps", "4", "--warmup", "1", "--no-cpu",
+           "--batch", "4096", "--input-batches", "2", "--coupled-batch", "512",
+           "--settle-seconds", "0.02"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["qp_status_ok_fraction"] == 1.0
+    assert d["coupled"]["exchange"].startswith("RCCL")
+    assert d["coupled"]["qp_status_ok_fraction"] == 1.0
