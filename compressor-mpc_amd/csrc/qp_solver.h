@@ -129,7 +129,10 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
 // for larger N they are rebuilt from (j, side) where they are used
 // (Qp::normal, the same vector bit for bit), which frees 2 N^2 registers per
 // working set: the centralized nV = 8 solve then needs no scratch.
-template <int N, bool SN = (N <= 6)>
+#ifndef CMPC_WSET_STORE_MAX
+#define CMPC_WSET_STORE_MAX 6  // largest N whose working sets store their normals
+#endif
+template <int N, bool SN = (N <= CMPC_WSET_STORE_MAX)>
 struct WSet {
   int K;
   int j[N], side[N];
@@ -340,7 +343,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
                          WSet<N>* wc = nullptr, uint32_t* wc_ws = nullptr) {
   WSet<N> Wl;
   WSet<N>& W = CACHE ? *wc : Wl;
-  constexpr bool SN = (N <= 6);
+  constexpr bool SN = (N <= CMPC_WSET_STORE_MAX);
   const bool cached = CACHE && pd && *wc_ws == ws_in;
   bool fact_ok = cached;  // W.L, W.D are the factors of the current slots
   o.status = CMPC_QP_OK;
