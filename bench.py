@@ -458,8 +458,7 @@ def main():
                     ctx.observe_apply()
                 ctx.synchronize()
                 t_full = (time.perf_counter() - t0) / reps
-                obs_kernels = {"observe_post": kms(cmpc.CMPC_KERNEL_OBSERVE_POST),
-                               "produce_per_qp": kms(cmpc.CMPC_KERNEL_PRODUCE),
+                obs_kernels = {"observe_post_produce": kms(cmpc.CMPC_KERNEL_PRODUCE),
                                "build": kms(cmpc.CMPC_KERNEL_BUILD), "iterate": kms(cmpc.CMPC_KERNEL_ITERATE),
                                "observe_prior": kms(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
                 ctx.enable_timing(False)
@@ -506,8 +505,7 @@ def main():
                         loop.step()
                     torch.cuda.synchronize(local)
                     lk = lambda k: loop.ctx.kernel_time(k)[0] / max(loop.ctx.kernel_time(k)[1], 1)
-                    plant_kernels = {"observe_post": lk(cmpc.CMPC_KERNEL_OBSERVE_POST),
-                                     "produce_per_qp": lk(cmpc.CMPC_KERNEL_PRODUCE),
+                    plant_kernels = {"observe_post_produce": lk(cmpc.CMPC_KERNEL_PRODUCE),
                                      "build": lk(cmpc.CMPC_KERNEL_BUILD), "iterate": lk(cmpc.CMPC_KERNEL_ITERATE),
                                      "observe_prior": lk(cmpc.CMPC_KERNEL_OBSERVE_PRIOR)}
                     loop.ctx.enable_timing(False)

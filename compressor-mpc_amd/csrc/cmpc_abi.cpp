@@ -717,8 +717,9 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
 
 int cmpc_observer_len(const cmpc_ctx* c) { return c ? c->obs_len : 0; }
 
-// linearise every QP slot at its own x_hat (observer state) and store C
-static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) {
+// linearise every QP slot at its own x_hat (observer state) and store C;
+// with_post: the a-posteriori update of each slot first, in the same kernel
+static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y, bool with_post) {
   ProduceParams P;
   int no = 0;
   int io[CMPC_MAX_S_PRODUCE * CMPC_MAX_INPUTS], oi[CMPC_MAX_S_PRODUCE * 4];
@@ -747,6 +748,11 @@ static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y) 
   P.c_stride = c->obs_len;
   P.u_full = u_full;
   P.y = y;
+  if (with_post) {
+    P.obs_M = c->d_obsM;
+    P.obs = c->obs;
+    P.obs_ntot = c->L.ntot;
+  }
   c->lin_bound = nullptr;
   TimedLaunch tl(c, CMPC_KERNEL_PRODUCE);
   if (tl.begin()) return -1;
@@ -785,7 +791,7 @@ int cmpc_observer_init(cmpc_ctx* c, int plant, double p_in, double p_out, double
   P.y = y_init;
   if (cmpc_launch_observer(P, CMPC_OBS_INIT, c->stream)) return fail("observer init launch failed");
   if (check_launch("observer init kernel")) return -1;
-  return observer_produce(c, u_full, y_init);  // Initialize: Update(x_init, full_u_old)
+  return observer_produce(c, u_full, y_init, false);  // Initialize: Update(x_init, full_u_old)
 }
 
 int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
@@ -794,15 +800,9 @@ int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
   if (c->obs_plant < 0) return fail("cmpc_observe_step: call cmpc_observer_init first");
   HIP_TRY(hipSetDevice(c->device));
   if (observer_upload_M(c)) return -1;
-  ObserverParams P;
-  observer_params(c, &P);
-  P.y = y;
-  TimedLaunch tl(c, CMPC_KERNEL_OBSERVE_POST);
-  if (tl.begin()) return -1;
-  if (cmpc_launch_observer(P, CMPC_OBS_POST, c->stream)) return fail("observer launch failed");
-  if (check_launch("observer a-posteriori kernel")) return -1;
-  if (tl.end()) return -1;
-  return observer_produce(c, u_full, y);
+  // ObserveAPosteriori + Update: one kernel (the producer runs the
+  // a-posteriori update of its slot first; cmpc_obs_post_kernel's arithmetic)
+  return observer_produce(c, u_full, y, true);
 }
 
 int cmpc_observe_apply(cmpc_ctx* c) {

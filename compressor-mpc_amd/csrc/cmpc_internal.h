@@ -147,11 +147,17 @@ struct ProduceParams {
   // spans dx_aug entries [rb[k], rb[k] + rlen[k]), logical entry i stored at
   // rb[k] + (i + rot[k]) mod rlen[k]
   int nring, rb[CMPC_ND_MAX], rlen[CMPC_ND_MAX], rot[CMPC_ND_MAX];
+  // per-QP mode, cmpc_observe_step: the observer's a-posteriori update of the
+  // slot (ObserveAPosteriori, cmpc_obs_post_kernel's arithmetic) runs first in
+  // the same kernel, x = the observer rows (x_hat, then dx of obs_ntot
+  // entries, y_old, C): obs_M = S x nobs x n_outputs gains, or null
+  const double* obs_M;
+  double* obs;  // the observer rows (x above, writable)
+  int obs_ntot;
 };
 
 // Observer kernels (observer.hip)
 #define CMPC_OBS_INIT 0
-#define CMPC_OBS_POST 1
 #define CMPC_OBS_PRIOR 2
 struct ObserverParams {
   double* obs;              // nqp * obs_len state rows

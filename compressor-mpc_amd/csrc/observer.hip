@@ -4,7 +4,7 @@
 //   iterations -> observe a priori + u_old update
 // stays on the device, the observer state resident in HBM between steps.
 //
-//   Observer::ObserveAPosteriori            libs/observer.cc:27-44
+//   Observer::ObserveAPosteriori            libs/observer.cc:27-44 (in produce.hip)
 //   x_ += (GenerateInitialQP)               libs/distributed_controller.cc:80
 //   Observer::ObserveAPriori                libs/observer.cc:8-22, with
 //     AdjustFirstDelayedStates / AdjustAppliedInput (include/aug_lin_sys.h:129-163),
@@ -51,52 +51,9 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_init_kernel(ObserverPara
   if (lane < P.n_out) st[P.ns + P.ntot + lane] = P.y[(size_t)b * P.n_out + lane];
 }
 
-// a posteriori: four QPs per wave, one 16-lane row each (nobs <= 16).  All
-// loads are issued up front (dims are compile-time), the cross-lane values
-// move by lane shuffles inside the row.
-template <int NS, int NO>
-__global__ __launch_bounds__(64 * kWaves) void cmpc_obs_post_kernel(ObserverParams P) {
-  constexpr int ND = NO;  // disturbance states = outputs (C = [C_plant | I])
-  constexpr int NOBS = NS + ND;
-  static_assert(NOBS <= 16, "one 16-lane row per QP");
-  const int lane = threadIdx.x & 63;
-  const int row = lane >> 4, l = lane & 15, base = lane & ~15;
-  const int q = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4 + row;
-  const bool valid = q < P.nqp;
-  const int qq = valid ? q : P.nqp - 1;  // (idle rows read a valid slot, store nothing)
-  const int b = qq / P.S, s = qq - b * P.S;
-  double* st = P.obs + (size_t)qq * P.obs_len;
-  double* dx = st + NS;
-  double* yo = dx + P.ntot;
-  const double* C = yo + NO;
-  const double* y = P.y + (size_t)b * NO;
-  const double* M = P.M + (size_t)s * NOBS * NO;
-  // loads: dx[l] and M row l (lanes < nobs); C row l, y, y_old (lanes < n_out)
-  const double dxl = (l < NOBS) ? dx[l] : 0.0;
-  const double xl = (l < NS) ? st[l] : 0.0;
-  double mrow[NO], crow[NS];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) mrow[o] = (l < NOBS) ? M[l * NO + o] : 0.0;
-  const int lc = l < NO ? l : 0;
-#pragma unroll
-  for (int j = 0; j < NS; ++j) crow[j] = C[lc * NS + j];
-  const double yl = y[lc], yol = yo[lc];
-  // innovation v = (y - y_old) - C dx[:nobs]   (lane o < n_out)
-  double t = 0.0;
-#pragma unroll
-  for (int j = 0; j < NS; ++j) t += crow[j] * __shfl(dxl, base + j, 64);
-  t = t + __shfl(dxl, base + NS + lc, 64);
-  const double v = (yl - yol) - t;
-  // dx[:nobs] += M v   (lane k);  y_old = y;  x_ += dx[:ns]
-  double acc = 0.0;
-#pragma unroll
-  for (int o = 0; o < NO; ++o) acc += mrow[o] * __shfl(v, base + o, 64);
-  const double dn = dxl + acc;
-  if (!valid) return;
-  if (l < NOBS) dx[l] = dn;
-  if (l < NS) st[l] = xl + dn;
-  if (l < NO) yo[l] = yl;
-}
+// a posteriori (ObserveAPosteriori, libs/observer.cc:27-44): fused into the
+// per-QP producer (produce.hip, cmpc_observe_step), which runs it on the same
+// 16-lane rows before linearising at the updated x_hat.
 
 // a priori + u_old update, four QPs per wave (one 16-lane row each).
 // The delay blocks of dx are rings: block k's logical state i (i < D - 1,
@@ -219,17 +176,6 @@ int cmpc_launch_observer(const ObserverParams& P, int mode, void* stream) {
     case CMPC_OBS_INIT:
       hipLaunchKernelGGL(cmpc_obs_init_kernel, dim3(grid), dim3(64 * kWaves), 0, s, P);
       return 0;
-    case CMPC_OBS_POST: {
-      if (!cmpc_obs_supported(P.ns, P.n_out, P.ndist, P.ntot - P.nobs, P.nd, P.nu_tot)) return -1;
-      const int g4 = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);
-      if (P.ns == 11 && P.n_out == 4 && P.ndist == 4)
-        cmpc_launch((cmpc_obs_post_kernel<11, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
-      else if (P.ns == 10 && P.n_out == 4 && P.ndist == 4)
-        cmpc_launch((cmpc_obs_post_kernel<10, 4>), dim3(g4), dim3(64 * kWaves), 0, s, P);
-      else
-        return -1;
-      return 0;
-    }
     case CMPC_OBS_PRIOR: {
       if (!cmpc_obs_supported(P.ns, P.n_out, P.ndist, P.ntot - P.nobs, P.nd, P.nu_tot)) return -1;
       const int g = (P.nqp + 4 * kWaves - 1) / (4 * kWaves);

@@ -109,7 +109,51 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   }
   __syncthreads();
 
-  if (valid && l < ns) xs[l] = P.per_qp ? P.x[(size_t)unit * P.x_stride + l] : P.x[(size_t)b * ns + l];
+  // cmpc_observe_step: ObserveAPosteriori of the slot first (libs/observer.cc:
+  // 27-44; the same loads, shuffles and arithmetic as cmpc_obs_post_kernel),
+  // then the linearisation at the updated x_hat.  The updated disturbance
+  // states of dx reach the record's observer tail from registers (dnd).
+  const bool post = P.per_qp && P.obs_M;
+  double xq = 0.0, dnd = 0.0;
+  if (post) {
+    constexpr int NO = 4, NOBS = ns + NO;  // disturbance states = outputs (C = [C_plant | I])
+    const int base = lane & ~(kLanes - 1);
+    const int qq = valid ? unit : P.B * P.S - 1;
+    const int bq = qq / P.S, sq = qq - bq * P.S;
+    double* st = P.obs + (size_t)qq * P.x_stride;
+    double* dxo = st + ns;
+    double* yo = dxo + P.obs_ntot;
+    const double* Cq = yo + NO;
+    const double* yq = P.y + (size_t)bq * NO;
+    const double* Mq = P.obs_M + (size_t)sq * NOBS * NO;
+    const double dxl = (l < NOBS) ? dxo[l] : 0.0;
+    const double xl = (l < ns) ? st[l] : 0.0;
+    double mrow[NO], crow[ns];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) mrow[o] = (l < NOBS) ? Mq[l * NO + o] : 0.0;
+    const int lc = l < NO ? l : 0;
+#pragma unroll
+    for (int j = 0; j < ns; ++j) crow[j] = Cq[lc * ns + j];
+    const double yl = yq[lc], yol = yo[lc];
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < ns; ++j) t += crow[j] * __shfl(dxl, base + j, 64);
+    t = t + __shfl(dxl, base + ns + lc, 64);
+    const double v = (yl - yol) - t;
+    double acc = 0.0;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc += mrow[o] * __shfl(v, base + o, 64);
+    const double dn = dxl + acc;
+    xq = xl + dn;
+    dnd = __shfl(dn, base + ns + lc, 64);
+    if (valid) {
+      if (l < NOBS) dxo[l] = dn;
+      if (l < ns) st[l] = xq;
+      if (l < NO) yo[l] = yl;
+    }
+  }
+  if (valid && l < ns)
+    xs[l] = post ? xq : P.per_qp ? P.x[(size_t)unit * P.x_stride + l] : P.x[(size_t)b * ns + l];
   if (valid && l < ni) us[l] = P.u_full[(size_t)b * ni + l];
   for (int e = l; e < ns * ns; e += kLanes) A[e] = 0.0;  // the row clears, its lane 0
   for (int e = l; e < ns * 4; e += kLanes) {             // writes the nonzeros
@@ -211,7 +255,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + u * kLanes;
-        v[u] = (dx && e < P.naug) ? dx[dmap[e]] : 0.0;
+        v[u] = (post && e < 4) ? dnd : (dx && e < P.naug) ? dx[dmap[e]] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)

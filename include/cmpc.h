@@ -184,8 +184,8 @@ int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
  * to time only those kernels (the others launch without events). */
 #define CMPC_KERNEL_BUILD 0
 #define CMPC_KERNEL_ITERATE 1         /* cmpc_iterate, cmpc_coupled_iterate */
-#define CMPC_KERNEL_PRODUCE 2         /* cmpc_produce_lin, the per-QP producer of cmpc_observe_step */
-#define CMPC_KERNEL_OBSERVE_POST 3    /* a posteriori part of cmpc_observe_step */
+#define CMPC_KERNEL_PRODUCE 2         /* cmpc_produce_lin; cmpc_observe_step (a posteriori + per-QP producer, one kernel) */
+#define CMPC_KERNEL_OBSERVE_POST 3    /* no launches since the a posteriori update runs in the producer (kept for the numbering) */
 #define CMPC_KERNEL_OBSERVE_PRIOR 4   /* cmpc_observe_apply */
 #define CMPC_KERNEL_COUNT 5
 #define CMPC_TIME_ONLY(kernel) (2 << (kernel))
