@@ -801,7 +801,7 @@ int cmpc_observe_step(cmpc_ctx* c, const double* u_full, const double* y) {
   HIP_TRY(hipSetDevice(c->device));
   if (observer_upload_M(c)) return -1;
   // ObserveAPosteriori + Update: one kernel (the producer runs the
-  // a-posteriori update of its slot first; cmpc_obs_post_kernel's arithmetic)
+  // a-posteriori update of its slot first, in or_observe_post's order)
   return observer_produce(c, u_full, y, true);
 }
 

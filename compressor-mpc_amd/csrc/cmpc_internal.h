@@ -148,7 +148,7 @@ struct ProduceParams {
   // rb[k] + (i + rot[k]) mod rlen[k]
   int nring, rb[CMPC_ND_MAX], rlen[CMPC_ND_MAX], rot[CMPC_ND_MAX];
   // per-QP mode, cmpc_observe_step: the observer's a-posteriori update of the
-  // slot (ObserveAPosteriori, cmpc_obs_post_kernel's arithmetic) runs first in
+  // slot (ObserveAPosteriori, in or_observe_post's arithmetic order) runs first in
   // the same kernel, x = the observer rows (x_hat, then dx of obs_ntot
   // entries, y_old, C): obs_M = S x nobs x n_outputs gains, or null
   const double* obs_M;

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams
   __syncthreads();
 
   // cmpc_observe_step: ObserveAPosteriori of the slot first (libs/observer.cc:
-  // 27-44; the same loads, shuffles and arithmetic as cmpc_obs_post_kernel),
+  // 27-44; the arithmetic order of oracle/or_observer.c or_observe_post),
   // then the linearisation at the updated x_hat.  The updated disturbance
   // states of dx reach the record's observer tail from registers (dnd).
   const bool post = P.per_qp && P.obs_M;
