@@ -157,3 +157,21 @@ def test_row_kernel_ring_protocol(p):
     assert errs == 0
     assert (ring > 0) == (p > 2 * 40 + 1)
     assert nseg <= 16
+
+
+def test_row_kernel_ring_protocol_random_delays():
+    """The same emulation over random horizons, delays, move counts and
+    unrolls (the kernel's and the others the code supports): every read
+    returns the value written for it, with or without rings."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ring_protocol_check as rp
+    rng = np.random.default_rng(7)
+    for _ in range(300):
+        p = int(rng.integers(2, 260))
+        D = int(rng.integers(1, p + 5))
+        M = int(rng.integers(1, 3))
+        U = int(rng.choice([rp.KERNEL_U, 4, 5]))
+        errs, ring, _ = rp.check(p, D, M=M, U=U)
+        assert errs == 0, (p, D, M, U)
+        assert (ring > 0) == ((M - 1) + max(0, p - D) > D + M), (p, D, M)

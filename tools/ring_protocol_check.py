@@ -6,9 +6,16 @@ wrap), the move-k gather reader of step s >= D reads entry (m - 1 - k) + s - D,
 with the kernel's segment bounds (D, p - D, the wraps) and its unrolled
 blocks.  Checks that every read returns h_{s-k-D} (zero before the line
 starts) for horizons up to the 16-bound limit.  Used by tests/test_abi.py."""
+import os
+import re
+
+# the kernel's horizon unroll (CMPC_ROWS_U, cmpc_internal.h)
+KERNEL_U = int(re.search(r"#define CMPC_ROWS_U (\d+)", open(os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "..", "compressor-mpc_amd", "csrc",
+    "cmpc_internal.h")).read()).group(1))
 
 
-def check(p, D, M=2, U=4):
+def check(p, D, M=2, U=KERNEL_U):
     full = (M - 1) + max(0, p - D)
     ring = D + M if full > D + M else 0
     L = ring if ring else full
