@@ -350,6 +350,15 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
   if (L.nuo != (d.S - 1) * d.nu && d.S != 1)
     return fail("nu_tot must equal S * nu (each sub-controller owns nu inputs), or S = 1");
   if (L.nd > CMPC_ND_MAX) return fail("more than 4 delayed inputs");
+  // A one-step delay with several delayed inputs: the reference's BComposite
+  // (libs/aug_lin_sys.cc:189-197) places such an input at index
+  // n_delayed_inputs + (sum of the earlier blocks' D - 1) - 1 of the
+  // augmented state, which is another input's delay state (only a single
+  // delayed input gets its own slot).  That mapping is not reproduced.
+  for (int i = 0; i < d.nu_tot; ++i)
+    if (d.delay[i] == 1 && L.nd > 1)
+      return fail("a delay of one step with several delayed inputs: the reference's BComposite "
+                  "maps it onto another input's delay state (aug_lin_sys.cc:189-197); not supported");
   if (d.ns + d.nu_tot > 15) return fail("ns + nu_tot must be <= 15 (16-lane DPP rows)");
   if (d.m * d.nu_tot + 1 > 16) return fail("m * nu_tot + 1 must be <= 16 (gather lanes of a DPP row)");
   if (d.ny > 4) return fail("ny > 4 is not instantiated in the build kernel (one DPP row per output)");
@@ -1388,8 +1397,8 @@ int cmpc_build(cmpc_ctx* c) {
   int rc = -1;
   // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
   // than the one-QP-per-wave kernel for every plant/controller type at
-  // p = 20, 50, 100, 200: tools/gpu_config_sweep.sh, tools/gpu_long_horizon.sh,
-  // DESIGN.md §3.0) and the batch gives it at least one wave per SIMD; else
+  // p = 20, 50, 100, 200: tools/gpu_build_table.sh) and the
+  // batch gives it at least one wave per SIMD; else
   // the one-QP-per-wave kernel, which has four times the waves for a small
   // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
   const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;

@@ -52,6 +52,19 @@ def test_layout_rejects_bad_dims():
     assert b"invalid" in load_library().cmpc_last_error()
 
 
+def test_one_step_delay_with_two_delayed_inputs_rejected():
+    """The reference's BComposite (aug_lin_sys.cc:189-197) maps a one-step
+    delay onto another input's delay state when two inputs are delayed; the
+    library refuses such dimensions instead of reproducing that (no GPU is
+    touched: the dimensions are checked first)."""
+    import dataclasses
+    cfg = dataclasses.replace(reference_config("par", "coop", p=50), delays=(0, 1, 0, 40))
+    d = CmpcDims.from_config(cfg, 4)
+    ctx = ctypes.c_void_p()
+    assert load_library().cmpc_create(ctypes.byref(ctx), ctypes.byref(d), 0) != 0
+    assert b"one step" in load_library().cmpc_last_error()
+
+
 def test_empty_batch_rejected_or_noop():
     """Edge cases of the batch size: an empty batch is an invalid dimension
     set (B < 1, like the reference's fixed-size Eigen types, which have no

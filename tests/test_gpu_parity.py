@@ -108,6 +108,43 @@ def test_gpu_build_matches_oracle(plant, ctype, p, variant):
             np.testing.assert_allclose(G[q], Go[q], rtol=0, atol=1e-11 * max(sG, 1e-6 * sH))
 
 
+# delays other than the reference plants' (0, 40, 0, 40): other segment
+# bounds, rings with other wrap steps, two-step delays and one of p - 1 (a
+# one-step delay with two delayed inputs is rejected: test_abi.py)
+OTHER_DELAYS = [("par", "coop", 50, (0, 10, 0, 25)), ("par", "coop", 100, (0, 30, 0, 60)),
+                ("par", "cent", 120, (0, 45, 0, 45)), ("ser", "coop", 80, (0, 15, 0, 50)),
+                ("par", "ncoop", 64, (0, 2, 0, 63)), ("par", "coop", 50, (0, 40, 0, 2))]
+
+
+@pytest.mark.parametrize("variant", [cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_ROWS])
+@pytest.mark.parametrize("plant,ctype,p,delays", OTHER_DELAYS)
+def test_gpu_build_other_delays_match_oracle(plant, ctype, p, delays, variant):
+    """Both build kernels against the oracle for input delays the reference
+    plants do not use (the delay lines, segment bounds and ring wraps of the
+    row kernel are runtime parameters)."""
+    import dataclasses
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = dataclasses.replace(cmpc.reference_config(plant, ctype, p=p), delays=tuple(delays))
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 47
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=23 + p)
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        ctx.set_build_variant(variant)
+        ctx.build()
+        assert ctx.last_build_kernel() == variant
+        H, f, G = ctx.download_qp()
+    Ho, fo, Go = oracle_qps(cfg, arr, lin, u_old)
+    assert np.all(np.abs(H - np.transpose(H, (0, 2, 1))) == 0)
+    for q in range(B * cfg.S):
+        sH = np.abs(Ho[q]).max()
+        np.testing.assert_allclose(H[q], Ho[q], rtol=0, atol=1e-11 * sH)
+        sf = max(np.abs(fo[q]).max(), 1e-300)
+        np.testing.assert_allclose(f[q], fo[q], rtol=0, atol=1e-10 * max(sf, 1e-6 * sH))
+        if cfg.nVo:
+            sG = max(np.abs(Go[q]).max(), 1e-300)
+            np.testing.assert_allclose(G[q], Go[q], rtol=0, atol=1e-11 * max(sG, 1e-6 * sH))
+
+
 @pytest.mark.parametrize("plant,ctype,p", [("par", "coop", 50), ("par", "cent", 50),
                                            ("ser", "coop", 100), ("par", "coop", 20),
                                            ("par", "coop", 100), ("par", "cent", 200),
