@@ -267,19 +267,15 @@ def compare_step(B, S, K, dev, orc, margin, excused):
     return diff & ~flag & ~excused, diff & (flag | excused)
 
 
-@pytest.mark.parametrize("plant,ctype,p,K", STEP_CASES)
-def test_gpu_step_matches_oracle(plant, ctype, p, K):
+def _step_parity(cfg, setup, K, B=96, seed=100):
     """Three closed-loop steps (state persists: ws, du_old, u_old with the
     first move applied), device and oracle each on their own state: plans
     within tolerance, statuses, nWSR, working sets and the working-set change
     sequences of every Jacobi iteration bit-exact, except scenarios the
     oracle flags as near-ties (decision margin < 1e-9, or_qp.c), which are
     counted and printed."""
-    _, setup, _, _ = setup_for(plant, ctype)
-    cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
-    B = 96
-    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=100 + p)
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=seed)
     o_u, o_du, o_ws = u_old.copy(), du_old.copy(), ws.copy()
     dims = CmpcDims.from_config(cfg, B)
     nq = B * cfg.S
@@ -309,6 +305,30 @@ def test_gpu_step_matches_oracle(plant, ctype, p, K):
             keep = np.repeat(~excused, cfg.S)
             np.testing.assert_allclose(du[keep], odu[keep], rtol=1e-9, atol=1e-10)
             np.testing.assert_allclose(u_g[keep], o_u[keep], rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("plant,ctype,p,K", STEP_CASES)
+def test_gpu_step_matches_oracle(plant, ctype, p, K):
+    """_step_parity on the reference plants' configurations."""
+    _, setup, _, _ = setup_for(plant, ctype)
+    _step_parity(cmpc.reference_config(plant, ctype, p=p), setup, K, seed=100 + p)
+
+
+# other delays and move counts: m = 1 (nV = nu) and m = 3 (the one-QP-per-wave
+# build kernel, nV = 6 solves)
+OTHER_STEP_CASES = [("par", "coop", 50, 2, (0, 10, 0, 25), 9), ("par", "coop", 120, 2, (0, 45, 0, 45), 9),
+                    ("ser", "coop", 80, 2, (0, 15, 0, 50), 5), ("par", "coop", 50, 1, (0, 40, 0, 40), 9),
+                    ("par", "coop", 30, 3, (0, 40, 0, 40), 9), ("par", "ncoop", 64, 2, (0, 2, 0, 63), 1)]
+
+
+@pytest.mark.parametrize("plant,ctype,p,m,delays,K", OTHER_STEP_CASES)
+def test_gpu_step_other_dims_matches_oracle(plant, ctype, p, m, delays, K):
+    """_step_parity for input delays and move counts the reference plants do
+    not use."""
+    import dataclasses
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = dataclasses.replace(cmpc.reference_config(plant, ctype, p=p, m=m), delays=tuple(delays))
+    _step_parity(cfg, setup, K, seed=300 + p + m)
 
 
 def test_gpu_step_matches_oracle_headline_size():
