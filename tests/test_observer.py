@@ -189,7 +189,9 @@ def lin_records(cfg, dims, L, xh, u_full, dx, y):
     # B*S not a multiple of the 16 QPs per a-priori workgroup: the tail groups
     ("par", "coop", 37, None), ("ser", "cent", 37, None),
     # longer delay lines (118 and 138 delay-block states; rings of 59 and 69)
-    ("par", "coop", 37, (0, 60, 0, 60)), ("par", "coop", 21, (0, 70, 0, 70))])
+    ("par", "coop", 37, (0, 60, 0, 60)), ("par", "coop", 21, (0, 70, 0, 70)),
+    # unequal delays: rings of different lengths, a one-entry ring
+    ("par", "coop", 37, (0, 2, 0, 25)), ("ser", "coop", 29, (0, 33, 0, 9))])
 def test_gpu_observer_kernels_match_oracle(plant, ctype, B, delays):
     cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, 20, B, 5, delays=delays)
     nq = B * cfg.S
