@@ -113,7 +113,10 @@ def test_gpu_build_matches_oracle(plant, ctype, p, variant):
 # one-step delay with two delayed inputs is rejected: test_abi.py)
 OTHER_DELAYS = [("par", "coop", 50, (0, 10, 0, 25)), ("par", "coop", 100, (0, 30, 0, 60)),
                 ("par", "cent", 120, (0, 45, 0, 45)), ("ser", "coop", 80, (0, 15, 0, 50)),
-                ("par", "ncoop", 64, (0, 2, 0, 63)), ("par", "coop", 50, (0, 40, 0, 2))]
+                ("par", "ncoop", 64, (0, 2, 0, 63)), ("par", "coop", 50, (0, 40, 0, 2)),
+                # short horizons: delays beyond p, a one-step remainder block
+                ("par", "coop", 7, (0, 40, 0, 40)), ("par", "coop", 3, (0, 2, 0, 2)),
+                ("ser", "cent", 11, (0, 4, 0, 9))]
 
 
 @pytest.mark.parametrize("variant", [cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_ROWS])
