@@ -18,7 +18,7 @@ import numpy as np
 from . import _abi
 from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE,
                    CMPC_KERNEL_PRODUCE, CMPC_KERNEL_OBSERVE_POST, CMPC_KERNEL_OBSERVE_PRIOR, CMPC_QP_INFEASIBLE,
-                   CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
+                   CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_NONFINITE, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
                    CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
 from .configs import ControllerConfig, SetupFile, reference_config, reference_observer_gain, reference_setup
 from .problem import ControllerArrays, controller_arrays, plant_input_from_plans
@@ -27,7 +27,8 @@ __all__ = ["Context", "ControllerConfig", "SetupFile", "reference_config", "refe
            "reference_observer_gain", "controller_arrays",
            "plant_input_from_plans", "plant_lin_record", "plant_default", "plant_output",
            "layout_of", "rows_lds_model", "qp_solve_batch", "CMPC_APPLY_MOVE", "CMPC_TRACE", "CMPC_QP_OK",
-           "CMPC_QP_MAX_NWSR", "CMPC_QP_INFEASIBLE", "CMPC_QP_NOT_PD"]
+           "CMPC_QP_MAX_NWSR", "CMPC_QP_INFEASIBLE", "CMPC_QP_NOT_PD",
+           "CMPC_QP_NONFINITE"]
 
 
 def layout_of(dims: CmpcDims) -> CmpcLayout:

@@ -21,6 +21,7 @@ CMPC_QP_OK = 0
 CMPC_QP_MAX_NWSR = 1
 CMPC_QP_INFEASIBLE = 2
 CMPC_QP_NOT_PD = 3
+CMPC_QP_NONFINITE = 4
 
 CMPC_APPLY_MOVE = 1
 CMPC_TRACE = 2

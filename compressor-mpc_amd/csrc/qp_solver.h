@@ -602,6 +602,15 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
   o.ws = w;
   if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && fact_ok) ? w : kWsInvalid;
+  // a non-finite plan (a NaN or infinite gradient) fails like any other
+  // non-success: zero move (or_qp.c; checked before the bound fixing).  The
+  // cached factors stay valid: they depend on H and the working set only.
+  if (o.status == CMPC_QP_OK) {
+    bool fin = true;
+#pragma unroll
+    for (int r = 0; r < N; ++r) fin = fin && __builtin_isfinite(x[r]);
+    if (!fin) o.status = CMPC_QP_NONFINITE;
+  }
   if (o.status == CMPC_QP_OK) {
     // variables at an active bound are fixed exactly at it; the bound
     // constraints are bits j < N of the working-set word (side at 16 + j),

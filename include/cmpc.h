@@ -62,6 +62,7 @@ extern "C" {
 #define CMPC_QP_MAX_NWSR 1    /* > n_wsr_max working-set changes -> zero move */
 #define CMPC_QP_INFEASIBLE 2  /* -> zero move */
 #define CMPC_QP_NOT_PD 3      /* Hessian not positive definite -> zero move */
+#define CMPC_QP_NONFINITE 4   /* non-finite plan (NaN / infinite gradient) -> zero move */
 
 /* cmpc_iterate / cmpc_step flags */
 #define CMPC_APPLY_MOVE 1u    /* u_old += first move (UpdateUOld/SendUHelper) */

@@ -416,6 +416,13 @@ done:
       w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
     info->ws = w;
   }
+  /* a non-finite plan (a NaN or infinite gradient; a NaN Hessian is not PD)
+   * is a failure like any other: zero move (libs/mpc_qp_solver.cc:66-69);
+   * checked before the bound fixing */
+  if (status == CMPC_QP_OK)
+    for (int i = 0; i < n; ++i)
+      if (!isfinite(x[i])) status = CMPC_QP_NONFINITE;
+  info->status = status;
   /* variables at an active bound are fixed exactly at it (qpOASES treats
    * active bounds as fixed variables) */
   if (status == CMPC_QP_OK)

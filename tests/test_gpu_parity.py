@@ -230,6 +230,18 @@ def test_gpu_solver_status_paths():
     x, st, nchg, _, _, _ = cmpc.qp_solve_batch(H, g, lb, ub, lbA, ubA, nu)
     assert st[0] == cmpc.CMPC_QP_OK and st[1] == cmpc.CMPC_QP_INFEASIBLE
     assert st[2] == cmpc.CMPC_QP_NOT_PD
+    # non-finite gradients (a NaN, an infinite entry) and a NaN Hessian: zero
+    # move with a failure status, as the oracle
+    H2 = np.tile(np.diag([2.0, 3.0, 4.0, 5.0]), (3, 1, 1))
+    H2[2, 1, 1] = np.nan
+    g2 = np.array([[1.0, np.nan, 0.5, 0.2], [np.inf, -1.0, 0.5, 0.2], [1.0, -1.0, 0.5, 0.2]])
+    lb2 = np.full((3, n), -1.0); ub2 = np.full((3, n), 1.0)
+    lbA2 = np.full((3, n), -0.1); ubA2 = np.full((3, n), 0.1)
+    x2, st2, _, _, _, _ = cmpc.qp_solve_batch(H2, g2, lb2, ub2, lbA2, ubA2, nu)
+    for q in range(3):
+        xo, info = O.qp_solve(H2[q], g2[q], lb2[q], ub2[q], lbA2[q], ubA2[q], nu, 0)
+        assert st2[q] == info.status and st2[q] != cmpc.CMPC_QP_OK, (q, st2[q], info.status)
+        assert np.all(x2[q] == 0.0) and np.all(xo == 0.0)
     assert np.all(x[1] == 0) and np.all(x[2] == 0)
     # n_wsr cap: the unconstrained optimum violates several rate rows
     g3 = np.array([[-50.0, 60.0, 80.0, -90.0]])
