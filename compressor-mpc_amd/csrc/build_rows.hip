@@ -97,8 +97,11 @@
 // RING: some delayed input's hand-off line is a ring (RowsLayout::ring; p > 2 D + 1):
 // the wrap bookkeeping and the longer segment list only where needed, so the
 // bench kernel (p = 50) keeps its registers (167 VGPRs, no scratch).
-template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG, bool RING>
-__global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(CMPC_ROWS_WPE, CMPC_ROWS_WPE)))
+// WPE: waves per SIMD the register allocation targets (CMPC_ROWS_WPE = 3, 168
+// registers; 2 for layouts whose LDS admits no more than two waves per SIMD
+// anyway: 256 registers, no spills for ny = 4 / nV = 8 at long horizons)
+template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG, bool RING, int WPE = CMPC_ROWS_WPE>
+__global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -570,9 +573,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // ---------------------------------------------------------------------------
 // Waves per workgroup (4, or 2 where that holds 1.5x the resident waves;
 // cmpc_rows_waves_per_group in rows_layout.cpp).
-template <int NS, int NY, int NU, int M, int WPG, bool RING>
+template <int NS, int NY, int NU, int M, int WPG, bool RING, int WPE = CMPC_ROWS_WPE>
 static int rows_launch(const BuildParams& P, hipStream_t s) {
-  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG, RING>;
+  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG, RING, WPE>;
   const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * WPG);
   if (lds > 160 * 1024) return -1;
   if (lds > 64 * 1024)
@@ -582,7 +585,7 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPG, lds) != hipSuccess ||
       per_cu < 1)
     per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
-  per_cu = std::min(per_cu, std::max(1, 4 * CMPC_ROWS_WPE / WPG));  // ablation: fewer waves per SIMD
+  per_cu = std::min(per_cu, std::max(1, 4 * WPE / WPG));  // the register budget's waves per SIMD
   // the occupancy query counts the requested LDS only; the measured
   // allocation model (rows_layout.cpp) can allow fewer
   per_cu = std::max(1, std::min(per_cu, cmpc_rows_resident_groups(P.rows, WPG)));
@@ -592,13 +595,18 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   return 0;
 }
 
+// four-wave workgroups whose layout admits at most two waves per SIMD run the
+// 256-register (WPE = 2) instantiation
 #define ROWS_CASE(NS_, NY_, NU_, M_)                                                  \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
     const int w_ = cmpc_rows_waves_per_group(P.rows);                                  \
+    const bool two_ = w_ == 4 && cmpc_rows_resident_groups(P.rows, 4) * 4 <= 8;        \
     if (ring) {                                                                        \
+      if (two_) return rows_launch<NS_, NY_, NU_, M_, 4, true, 2>(P, s);               \
       if (w_ == 4) return rows_launch<NS_, NY_, NU_, M_, 4, true>(P, s);               \
       if (w_ == 2) return rows_launch<NS_, NY_, NU_, M_, 2, true>(P, s);               \
     } else {                                                                           \
+      if (two_) return rows_launch<NS_, NY_, NU_, M_, 4, false, 2>(P, s);              \
       if (w_ == 4) return rows_launch<NS_, NY_, NU_, M_, 4, false>(P, s);              \
       if (w_ == 2) return rows_launch<NS_, NY_, NU_, M_, 2, false>(P, s);              \
     }                                                                                  \
