@@ -10,9 +10,13 @@ move applied to u_old (cmpc_iterate with CMPC_APPLY_MOVE: SURVEY §8(a)
 a1-a13).  QP solves per step = B * S * K per GPU.
 
 Inputs are resident in HBM before the timed region: NB distinct synthetic
-batches are uploaded once and step i binds batch i % NB,
-so consecutive steps solve different QPs while the warm-start working sets
-persist, as in the reference's closed loop.
+batches of B scenarios are uploaded once, each with its own
+controller state (u_old, move plans, warm-start working sets).  Step i binds
+batch i % NB's records (cmpc_bind_lin) and state (cmpc_bind_state), so
+consecutive steps solve different QPs (the 327 MB of records per batch are
+read from HBM, not from the 256 MB Infinity Cache) and every QP is
+warm-started from its own scenario's previous step, as each reference
+controller hot-starts its own QProblem.
 
 Multi-GPU: one process per GPU (torch.distributed.run), scenarios sharded
 across ranks with no data-path collective (weak scaling); the barrier and
@@ -259,24 +263,39 @@ def main():
     arrays = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
     B, S, K, NB = args.batch, cfg.S, args.K, args.input_batches
     t0 = time.time()
-    batches = []
+    batches, states = [], []
     u_old = du_old = ws = None
+    dev = f"cuda:{local}"
     for b in range(NB):
         lin, u, du, w = synthetic_batch(cfg, B, seed=1002 + 101 * rank + b, n_distinct=min(B, 2048))
         if b == 0:
             u_old, du_old, ws, lin0 = u, du, w, lin
-        batches.append(torch.from_numpy(lin).to(f"cuda:{local}"))
+        batches.append(torch.from_numpy(lin).to(dev))
+        # each batch is its own set of B scenarios with its own controller
+        # state (u_old, move plans, warm-start working sets), resident in HBM
+        states.append(tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                            for a in (u, du, w.view(np.int32))))
     torch.cuda.synchronize()
     log(f"[rank {rank}] synthetic inputs: {NB} x {B} scenarios in {time.time() - t0:.1f} s")
 
     ctx = cmpc.Context(cfg, B, device=local)
     ctx.configure(arrays)
     ctx.set_state(u_old, du_old, ws)
-    ctx.bind_lin(batches[0].data_ptr())
-    ctx.build()
-    ctx.init_warmstart()
-    for i in range(args.warmup):
+
+    def bind(i):
+        """Step i runs on batch i % NB: its records and its own state, so every
+        QP is warm-started from its own scenario's previous step (the reference
+        hot-starts each controller's own QProblem, libs/mpc_qp_solver.cc:42-75)."""
+        st_ = states[i % NB]
         ctx.bind_lin(batches[i % NB].data_ptr())
+        ctx.bind_state(st_[0].data_ptr(), st_[1].data_ptr(), st_[2].data_ptr())
+
+    for b in range(NB):  # InitializeQPProblem of every batch's controllers
+        bind(b)
+        ctx.build()
+        ctx.init_warmstart()
+    for i in range(args.warmup):
+        bind(i)
         ctx.step(K, 0)
     ctx.synchronize()
     # clock settle (SURVEY §8(d): time the steady state): from a cold start the
@@ -284,7 +303,7 @@ def main():
     settle_steps, t_settle = 0, time.perf_counter()
     while time.perf_counter() - t_settle < args.settle_seconds:
         for _ in range(16):
-            ctx.bind_lin(batches[(args.warmup + settle_steps) % NB].data_ptr())
+            bind(args.warmup + settle_steps)
             ctx.step(K, 0)
             settle_steps += 1
         ctx.synchronize()
@@ -298,12 +317,14 @@ def main():
     # the roofline kernel (build) carries dispatch-stamped HIP events in the
     # timed steps; the iterate kernel is timed in its own pass afterwards.
     # The timed steps apply the first move (UpdateUOld):
-    # u_old moves from the batch's drawn state over the K timed steps (the
+    # each batch's u_old moves from its drawn state over the timed steps (the
     # warmup and settle steps leave it unchanged) and is restored after.
+    snap = [tuple(a.clone() for a in st_) for st_ in states]
+    torch.cuda.synchronize()
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
     for i in range(args.steps):
-        ctx.bind_lin(batches[(first + i) % NB].data_ptr())
+        bind(first + i)
         ctx.step(K, cmpc.CMPC_APPLY_MOVE)
     ctx.synchronize()
     torch.cuda.synchronize()
@@ -318,20 +339,31 @@ def main():
     elapsed_max = float(t.item())
 
     du, st, nw = ctx.download()
-    u_moved, _, ws_now = ctx.get_state()
-    u_drift = float(np.abs(u_moved - u_old).max())
+    u_drift = max(float((st_[0] - sn[0]).abs().max()) for st_, sn in zip(states, snap))
+    ws_now = states[(first + args.steps - 1) % NB][2].cpu().numpy()  # the last step's batch
 
-    # the iterate kernel's own time: the same step loop, events on the iterate
-    # only (after the headline measurement, untimed for `value`)
-    ctx.set_state(u_old, None, None)
+    def restore():
+        for st_, sn in zip(states, snap):
+            for a, a0 in zip(st_, sn):
+                a.copy_(a0)
+        torch.cuda.synchronize()
+
+    # the iterate kernel's own time: the same step loop from the same states,
+    # events on the iterate only (after the headline measurement, untimed for
+    # `value`)
+    restore()
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
     for i in range(args.steps):
-        ctx.bind_lin(batches[(first + args.steps + i) % NB].data_ptr())
+        bind(first + i)
         ctx.step(K, cmpc.CMPC_APPLY_MOVE)
     ctx.synchronize()
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     ctx.enable_timing(False)
-    ctx.set_state(u_old, None, None)
+    restore()
+    # the sections below run on the context's own state buffers
+    ctx.bind_state()
+    ctx.bind_lin(0)
+    ctx.set_state(u_old, du_old, ws)
 
     def warm():
         """Build launches on a resident batch for --settle-seconds, then the

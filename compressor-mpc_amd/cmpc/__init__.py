@@ -187,6 +187,13 @@ class Context:
         """Bind an external device-resident record array (0 = own buffer)."""
         check(self.lib.cmpc_bind_lin(self._h, ctypes.c_void_p(device_ptr or None)), "cmpc_bind_lin")
 
+    def bind_state(self, u_old_ptr: int = 0, du_old_ptr: int = 0, ws_ptr: int = 0):
+        """Bind external device-resident state arrays (u_old B*S x nu_tot f64,
+        du_old B*S x nV f64, ws B*S u32; all three, or 0 for the own buffers)."""
+        vp = lambda p: ctypes.c_void_p(p or None)
+        check(self.lib.cmpc_bind_state(self._h, vp(u_old_ptr), vp(du_old_ptr), vp(ws_ptr)),
+              "cmpc_bind_state")
+
     def produce_lin(self, x_ptr: int, u_full_ptr: int, y_ptr: int, dx_aug_ptr: int = 0,
                     Ts: float = 0.05, p_in: float = 1.0, p_out: float = 1.0):
         """Device producer (cmpc_produce_lin): linearise + discretise the plant

@@ -90,6 +90,7 @@ EXPORTS = (
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
+    "cmpc_bind_state",
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
     "cmpc_get_input", "cmpc_get_input_host", "cmpc_update_u", "cmpc_update_u_host",
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
@@ -144,6 +145,7 @@ def load_library(path: str = LIB_PATH):
         "cmpc_lin_device": ([c_void], c_void),
         "cmpc_download_lin": ([c_void, P(dbl)], ctypes.c_int),
         "cmpc_bind_lin": ([c_void, c_void], ctypes.c_int),
+        "cmpc_bind_state": ([c_void, c_void, c_void, c_void], ctypes.c_int),
         "cmpc_build": ([c_void], ctypes.c_int),
         "cmpc_set_build_variant": ([c_void, ctypes.c_int], ctypes.c_int),
         "cmpc_last_build_kernel": ([c_void], ctypes.c_int),

@@ -151,6 +151,10 @@ struct cmpc_ctx {
   double *lin = nullptr, *qp = nullptr, *cfg = nullptr, *u_old = nullptr, *du_old = nullptr,
          *du = nullptr;
   uint32_t* ws = nullptr;
+  // the context's own state buffers; u_old/du_old/ws above point at them
+  // unless cmpc_bind_state bound external ones
+  double *own_u_old = nullptr, *own_du_old = nullptr;
+  uint32_t* own_ws = nullptr;
   int32_t *status = nullptr, *nwsr = nullptr, *ntrace = nullptr;
   char* out_block = nullptr;  // du | status | nwsr in one allocation: one D2H for cmpc_download
   size_t out_st = 0, out_nw = 0, out_len = 0;  // byte offsets of status, nwsr; block length
@@ -411,6 +415,9 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
       hipMalloc(&c->du_old, sizeof(double) * n * L.nV) != hipSuccess ||
       hipMalloc(&c->ws, sizeof(uint32_t) * n) != hipSuccess)
     return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
+  c->own_u_old = c->u_old;
+  c->own_du_old = c->du_old;
+  c->own_ws = c->ws;
   {
     auto up16 = [](size_t v) { return (v + 15) / 16 * 16; };
     c->out_st = up16(sizeof(double) * n * L.nV);
@@ -448,8 +455,14 @@ int cmpc_destroy(cmpc_ctx* c) {
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   pinned_free(c->pin_in);
   pinned_free(c->pin_out);
-  void* bufs[] = {c->lin, c->qp, c->cfg, c->u_old, c->du_old, c->out_block,
-                  c->ws,  c->trace, c->ntrace, c->obs, c->d_obsM,
+  // own state buffers (bound external ones belong to the caller); before they
+  // are recorded (a failed create) the active pointers are the own ones
+  void* bufs[] = {c->lin, c->qp, c->cfg,
+                  c->own_u_old ? c->own_u_old : c->u_old,
+                  c->own_du_old ? c->own_du_old : c->du_old,
+                  c->out_block,
+                  c->own_ws ? c->own_ws : c->ws,
+                  c->trace, c->ntrace, c->obs, c->d_obsM,
                   c->stage};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -574,6 +587,32 @@ int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
       return fail("cmpc_bind_lin: records must be 16-byte aligned");
   }
   c->lin_bound = lin_device;
+  return 0;
+}
+
+int cmpc_bind_state(cmpc_ctx* c, double* u_old, double* du_old, uint32_t* ws) {
+  if (!c) return fail("null context");
+  const int nnull = !u_old + !du_old + !ws;
+  if (nnull == 3) {
+    c->u_old = c->own_u_old;
+    c->du_old = c->own_du_old;
+    c->ws = c->own_ws;
+    return 0;
+  }
+  if (nnull != 0) return fail("cmpc_bind_state: bind all three state arrays or none");
+  const void* ptrs[] = {u_old, du_old, ws};
+  for (const void* p : ptrs) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice ||
+        a.device != c->device)
+      return fail("cmpc_bind_state: not a device pointer on the context's device");
+  }
+  if (reinterpret_cast<uintptr_t>(u_old) % 8 || reinterpret_cast<uintptr_t>(du_old) % 8 ||
+      reinterpret_cast<uintptr_t>(ws) % 4)
+    return fail("cmpc_bind_state: misaligned state array");
+  c->u_old = u_old;
+  c->du_old = du_old;
+  c->ws = ws;
   return 0;
 }
 

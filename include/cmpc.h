@@ -130,6 +130,15 @@ int cmpc_set_reference(cmpc_ctx* ctx, int s, const double* y_ref /* p x ny */);
 int cmpc_set_state(cmpc_ctx* ctx, const double* u_old, const double* du_old,
                    const uint32_t* ws);
 int cmpc_get_state(cmpc_ctx* ctx, double* u_old, double* du_old, uint32_t* ws);
+/* Bind external device-resident state arrays (shapes as above, on the ctx
+ * device, 8-byte aligned): every later call reads and updates them in place
+ * of the context's own state, as if they were the context's.  All three
+ * pointers, or all NULL to re-bind the context's own buffers.  Lets one
+ * context serve several sets of B scenarios in rotation (cmpc_bind_lin for
+ * their records), each set warm-started from its own previous step, as each
+ * reference controller hot-starts its own QProblem (libs/mpc_qp_solver.cc:42-75). */
+int cmpc_bind_state(cmpc_ctx* ctx, double* u_old_device, double* du_old_device,
+                    uint32_t* ws_device);
 
 /* Inputs: B*S lin records from host memory (H2D copy on the ctx stream), or
  * written in place by a device-side producer through cmpc_lin_device(). */

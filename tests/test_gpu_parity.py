@@ -576,3 +576,64 @@ def test_gpu_build_auto_selects_kernel(ctype, p, B, expect):
         ctx.build()
         got = ctx.last_build_kernel()
     assert got == {"rows": cmpc.CMPC_BUILD_ROWS, "wave": cmpc.CMPC_BUILD_WAVE}[expect]
+
+
+def test_gpu_bound_state_rotation():
+    """cmpc_bind_state: one context serving two sets of scenarios in rotation
+    (records by cmpc_bind_lin, state by cmpc_bind_state, as bench.py does)
+    gives bit for bit what two contexts with their own state give; NULL
+    re-binds the context's own, untouched state."""
+    import torch
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B, K = 512, 9
+    sets = [synthetic_batch(cfg, B, seed=4100 + i, n_distinct=128) for i in range(2)]
+    # reference: one context per set, each with its own state
+    ref = []
+    for lin, u, du0, w in sets:
+        with make_ctx(cfg, arr, B, lin, u, du0, w) as ctx:
+            ctx.build()
+            ctx.init_warmstart()
+            outs = []
+            for _ in range(3):
+                ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+                outs.append(ctx.download())
+            ref.append((outs, ctx.get_state()))
+    # one context, the two sets bound in rotation
+    dev = "cuda:0"
+    lins = [torch.from_numpy(s[0]).to(dev) for s in sets]
+    states = [tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                    for a in (s[1], s[2], s[3].view(np.int32))) for s in sets]
+    u_own = np.full_like(sets[0][1], 0.25)
+    with cmpc.Context(cfg, B) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u_own, None, None)
+
+        def bind(i):
+            ctx.bind_lin(lins[i].data_ptr())
+            ctx.bind_state(*(a.data_ptr() for a in states[i]))
+
+        for i in range(2):
+            bind(i)
+            ctx.build()
+            ctx.init_warmstart()
+        got = [[], []]
+        for r in range(3):
+            for i in range(2):
+                bind(i)
+                ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+                got[i].append(ctx.download())
+        for i in range(2):
+            for (du, st, nw), (rdu, rst, rnw) in zip(got[i], ref[i][0]):
+                assert np.array_equal(du, rdu) and np.array_equal(st, rst) and np.array_equal(nw, rnw)
+            ru, rdu_old, rws = ref[i][1]
+            u_b, du_b, ws_b = (a.cpu().numpy() for a in states[i])
+            assert np.array_equal(u_b, ru) and np.array_equal(du_b, rdu_old)
+            assert np.array_equal(ws_b.view(np.uint32), rws)
+        assert not np.array_equal(ref[0][1][0], sets[0][1])  # the moves were applied
+        ctx.bind_state()
+        u_back, _, _ = ctx.get_state()
+        assert np.array_equal(u_back, u_own)
+        with pytest.raises(RuntimeError):
+            ctx.bind_state(states[0][0].data_ptr(), 0, 0)
