@@ -228,6 +228,9 @@ def main():
                          "profiler runs, so that every build launch in the trace is a headline one")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--coupled-batch", type=int, default=4096, help="config-4 scenarios per GPU")
+    ap.add_argument("--coupled-tiles", type=int, default=1,
+                    help="config-4 scenario tiles per GPU, each on its own stream: a tile's "
+                         "all-gather overlaps another tile's Jacobi iteration (1 = no overlap)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for the barrier and the max over ranks "
                          "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -565,7 +568,7 @@ def main():
         from cmpc.coupled import run_coupled_bench
         rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
                                steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds,
-                               force_collective=bool(dist))
+                               force_collective=bool(dist), tiles=args.coupled_tiles)
         tc = torch.tensor([rc["elapsed_s"]], dtype=torch.float64,
                           device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
         if dist:
@@ -582,9 +585,12 @@ def main():
                          else "local copy (world size 1)"),
             "note": "SURVEY config 4: S_total = 8 x world sub-controllers per scenario (synthetic "
                     "coupling, cmpc/coupled.py), 8 per GPU; step = build + K x (all-gather + "
-                    "coupled iteration), first move applied; per-GPU work grows with S_total "
-                    "(G_ext is nV x (S_total - 1) nV per QP); gather_ms from events in a "
-                    "separate pass"})
+                    "coupled iteration), first move applied; with tiles > 1 the scenarios run as "
+                    "that many tiles on their own streams, each tile's all-gather overlapping "
+                    "another tile's iteration (cmpc.coupled.CoupledPipeline; slower at world 1, "
+                    "DESIGN.md section 8); per-GPU work grows with S_total "
+                    "(G_ext is nV x (S_total - 1) nV per QP); gather_ms (summed over the tiles) "
+                    "from events in a separate pass"})
 
     ok_frac = float((st == 0).mean())
     active_frac = float((ws_now != 0).mean())

@@ -35,12 +35,14 @@ def coupling_weights(b, s, S_total: int) -> np.ndarray:
     return w[keep].reshape(w.shape[:-1] + (S_total - 1,))
 
 
-def synthetic_g_ext(G_local: np.ndarray, S_total: int, S_local: int, s_offset: int) -> np.ndarray:
+def synthetic_g_ext(G_local: np.ndarray, S_total: int, S_local: int, s_offset: int,
+                    b_offset: int = 0) -> np.ndarray:
     """Element-major G_ext [nV*(S_total-1)*nV][nqp] for this rank's QPs
-    (q = b*S_local + local index).  G_local: (nqp, nV, nVo=nV) from the build."""
+    (q = b*S_local + local index, scenarios b_offset + b for a tile of the
+    rank's scenarios).  G_local: (nqp, nV, nVo=nV) from the build."""
     nqp, nV, _ = G_local.shape
     q = np.arange(nqp)
-    b, sl = q // S_local, q % S_local
+    b, sl = b_offset + q // S_local, q % S_local
     w = coupling_weights(b, s_offset + sl, S_total)            # (nqp, S_total-1)
     out = np.einsum("qj,qav->ajvq", w, G_local)                # (nV, S_total-1, nV, nqp)
     return np.ascontiguousarray(out.reshape(nV * (S_total - 1) * nV, nqp))
@@ -88,6 +90,11 @@ class CoupledRank:
         nqp = ctx.B * ctx.cfg.S
         if nqp % S_local:
             raise ValueError("B*S must be a multiple of S_local")
+        # the kernel reads every other sub-controller's plan from du_all
+        # [S_total / S_local ranks][nqp][nV]: a layout with fewer ranks than
+        # that would read past the gathered plans
+        if S_local * world != S_total:
+            raise ValueError(f"S_total ({S_total}) must be S_local ({S_local}) x world ({world})")
         self.B = nqp // S_local
         nV = ctx.cfg.nV
         dev = G_ext.device
@@ -127,22 +134,95 @@ class CoupledRank:
             self.iterate(k == K - 1)
 
 
+class CoupledPipeline:
+    """One rank's share split into scenario tiles, each a CoupledRank on its
+    own context and HIP stream (overlap the gather with the
+    next scenario tile's solve).  Iteration k runs tile by tile: the
+    all-gather of tile t waits only for tile t's previous iteration, so it
+    overlaps the coupled iteration of the tile before it, and the tiles'
+    kernels may run side by side.  Every rank issues the collectives in the
+    same order (tile-major within an iteration).  The tiles are independent
+    sets of scenarios: the results equal one CoupledRank over all of them."""
+
+    def __init__(self, tiles, streams):
+        self.tiles, self.streams = tiles, streams
+
+    def step(self, K: int):
+        import torch
+        for cr, s in zip(self.tiles, self.streams):
+            with torch.cuda.stream(s):
+                cr.ctx.build()
+        for k in range(K):
+            for cr, s in zip(self.tiles, self.streams):
+                with torch.cuda.stream(s):
+                    cr.gather()
+                    cr.iterate(k == K - 1)
+
+
+def make_coupled_tiles(cfg, arr, lin, u_old, S_total: int, S_local: int, rank: int, world: int,
+                       device: int, tiles: int, group=None, force_collective: bool = False,
+                       build_variant: int = 0):
+    """Contexts, G_ext and CoupledRanks for `tiles` scenario tiles of one
+    rank's records (lin, u_old: B*S_local rows, q = b*S_local + i), each on
+    its own stream; build + warm-start initialisation done.  build_variant
+    (cmpc_set_build_variant) pins the build kernel: AUTO picks it by batch
+    size, and the two kernels' H, f, G differ in rounding."""
+    import torch
+
+    from . import Context
+    nqp = lin.shape[0]
+    B = nqp // S_local
+    if B % tiles:
+        raise ValueError("the rank's scenarios must split evenly into tiles")
+    bt = B // tiles
+    dev = f"cuda:{device}"
+    out, streams = [], []
+    for t in range(tiles):
+        rows = slice(t * bt * S_local, (t + 1) * bt * S_local)
+        s = torch.cuda.Stream(device=device) if tiles > 1 else torch.cuda.current_stream(device)
+        ctx = Context(cfg, bt * S_local // cfg.S, device=device)
+        try:
+            ctx.configure(arr)
+            if build_variant:
+                ctx.set_build_variant(build_variant)
+            n = bt * S_local
+            ctx.set_state(np.ascontiguousarray(u_old[rows]), np.zeros((n, cfg.nV)), np.zeros(n, np.uint32))
+            ctx.upload_lin(np.ascontiguousarray(lin[rows]))
+            ctx.build()
+            ctx.init_warmstart()
+            _, _, G = ctx.download_qp()
+            G_ext = torch.from_numpy(synthetic_g_ext(G, S_total, S_local, rank * S_local, t * bt)).to(dev)
+            with torch.cuda.stream(s):
+                out.append(CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group,
+                                       force_collective=force_collective))
+        except Exception:
+            ctx.close()
+            for cr in out:
+                cr.ctx.close()
+            raise
+        streams.append(s)
+    return out, streams
+
+
 def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: int = 4096, p: int = 50,
                       K: int = 9, steps: int = 20, warmup: int = 3, settle_seconds: float = 0.25,
-                      S_total: int = 0, group=None, force_collective: bool = False) -> dict:
+                      S_total: int = 0, group=None, force_collective: bool = False,
+                      tiles: int = 1) -> dict:
     """SURVEY config 4 on this rank: B scenarios x S_local sub-controllers
     (global indices rank * S_local + i of S_total = S_local * world), one
     step = build + K x (all-gather of the plans, coupled Jacobi iteration),
-    the first move applied in the last iteration.  The caller has set up the
-    process group (nccl = RCCL over xGMI between GPUs) when world > 1.
-    Returns this rank's timings; the whole-job value needs the max over ranks
-    of `elapsed_s` (the caller's barrier + all-reduce)."""
+    the first move applied in the last iteration; with tiles > 1 the
+    scenarios run as that many tiles on their own streams, each tile's
+    gather overlapping another tile's iteration (CoupledPipeline).  The
+    caller has set up the process group (nccl = RCCL over xGMI between GPUs)
+    when world > 1.  Returns this rank's timings; the whole-job value needs
+    the max over ranks of `elapsed_s` (the caller's barrier + all-reduce)."""
     import time
 
     import torch
     import torch.distributed as dist
 
-    from . import Context, controller_arrays, reference_config
+    from . import controller_arrays, reference_config
     from .configs import reference_setup
     from .synthetic import synthetic_batch
 
@@ -151,17 +231,10 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
     arr = controller_arrays(cfg, reference_setup("par", "coop"))
     nqp = B * S_local
     lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=500 + rank, n_distinct=1024)
-    ctx = Context(cfg, nqp // cfg.S, device=device)
+    crs, streams = make_coupled_tiles(cfg, arr, lin, u_old, S_total, S_local, rank, world, device,
+                                      tiles, group=group, force_collective=force_collective)
     try:
-        ctx.configure(arr)
-        ctx.set_state(u_old, np.zeros((nqp, cfg.nV)), np.zeros(nqp, np.uint32))
-        ctx.upload_lin(lin)
-        ctx.build()
-        ctx.init_warmstart()
-        _, _, G = ctx.download_qp()
-        G_ext = torch.from_numpy(synthetic_g_ext(G, S_total, S_local, rank * S_local)).to(f"cuda:{device}")
-        cr = CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group,
-                         force_collective=force_collective)
+        cr = CoupledPipeline(crs, streams)
         for _ in range(warmup):
             cr.step(K)
         torch.cuda.synchronize(device)
@@ -177,23 +250,29 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
             cr.step(K)
         torch.cuda.synchronize(device)
         elapsed = time.perf_counter() - t0
-        # the exchange alone: events around the gathers of a second pass
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(K)]
-        ctx.build()
+        # the exchange alone: events around each tile's gathers (on its
+        # stream) in a second pass; summed over the tiles per iteration
+        ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(K)] for _ in crs]
+        for c, s in zip(crs, streams):
+            with torch.cuda.stream(s):
+                c.ctx.build()
         for k in range(K):
-            ev[k][0].record()
-            cr.gather()
-            ev[k][1].record()
-            cr.iterate(k == K - 1)
+            for t, (c, s) in enumerate(zip(crs, streams)):
+                with torch.cuda.stream(s):
+                    ev[t][k][0].record()
+                    c.gather()
+                    ev[t][k][1].record()
+                    c.iterate(k == K - 1)
         torch.cuda.synchronize(device)
-        gather_ms = sum(a.elapsed_time(b) for a, b in ev) / K
-        _, st, _ = ctx.download()
+        gather_ms = sum(a.elapsed_time(b) for et in ev for a, b in et) / K
+        st = np.concatenate([c.ctx.download()[1] for c in crs])
         return {"elapsed_s": elapsed, "steps": steps, "qp_per_gpu": nqp, "S_total": S_total,
-                "S_local": S_local, "B": B, "p": p, "K": K,
-                "G_ext_MB_per_gpu": G_ext.numel() * 8 / 1e6,
+                "S_local": S_local, "B": B, "p": p, "K": K, "tiles": tiles,
+                "G_ext_MB_per_gpu": sum(c.G_ext.numel() for c in crs) * 8 / 1e6,
                 "gather_ms_per_iteration": gather_ms,
                 "gather_bytes_per_iteration": world * nqp * cfg.nV * 8,
                 "qp_status_ok_fraction": float((st == 0).mean())}
     finally:
-        ctx.close()
+        for c in crs:
+            c.ctx.close()

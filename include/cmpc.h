@@ -262,7 +262,9 @@ int cmpc_update_u_host(cmpc_ctx* ctx, const double* du_full);
  *   f_k = f + G_ext du_other,   du = SolveQP(H, f_k) warm-started
  * G_ext: device, [nV * (S_total-1) * nV][B*S_local] (element-major),
  *        column block j = the j-th other sub-controller in global order.
- * du_all: device, all-gathered plans [world][B][S_local][nV] (rank-major).
+ * du_all: device, all-gathered plans [world][B][S_local][nV] (rank-major),
+ *        world = S_total / S_local: the kernel reads all of it, so the
+ *        caller's buffer must hold S_total * B * nV doubles.
  * du_out: device [B*S_local][nV] or NULL: this rank's new plans (the next
  *        all-gather's input).  CMPC_APPLY_MOVE on the last iteration of a
  *        step applies the first move (UpdateUOld) and stores du_old.

@@ -292,3 +292,54 @@ def test_gpu_config4_full_size_matches_oracle():
     assert np.array_equal(st[qs], st_o)
     assert np.array_equal(ws_gpu[qs], ws)
     assert np.array_equal(du_gpu[qs], prev.reshape(-1, 4))
+
+
+@pytest.mark.gpu
+def test_gpu_coupled_pipeline_tiles_equal_one():
+    """CoupledPipeline (bench.py's config-4 section): the rank's scenarios as
+    two tiles on their own streams, each tile's gather overlapping the other
+    tile's iteration, give bit for bit the plans, statuses and working sets
+    of one CoupledRank over all scenarios (two steps, K = 9)."""
+    import torch
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.coupled import CoupledPipeline, make_coupled_tiles
+    from cmpc.synthetic import synthetic_batch
+    S_total, Bsc, K4 = 8, 512, 9
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    lin, u_old, _, _ = synthetic_batch(cfg, Bsc * S_total // cfg.S, seed=88, n_distinct=256)
+    res = []
+    for tiles in (1, 2):
+        crs, streams = make_coupled_tiles(cfg, arr, lin, u_old, S_total, S_total, 0, 1, 0, tiles,
+                                          build_variant=cmpc.CMPC_BUILD_ROWS)
+        try:
+            pipe = CoupledPipeline(crs, streams)
+            pipe.step(K4)
+            pipe.step(K4)
+            torch.cuda.synchronize()
+            du = np.concatenate([c.du_local.cpu().numpy() for c in crs])
+            st = np.concatenate([c.ctx.download()[1] for c in crs])
+            ws = np.concatenate([c.ctx.get_state()[2] for c in crs])
+        finally:
+            for c in crs:
+                c.ctx.close()
+        res.append((du, st, ws))
+    assert (res[0][1] == 0).mean() > 0.999
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+
+
+def test_coupled_rank_rejects_layout_beyond_gathered_plans():
+    """The coupled kernel reads the plans of all S_total sub-controllers from
+    du_all [S_total / S_local ranks]: a CoupledRank whose world does not
+    cover S_total (e.g. S_total = 64 with S_local = 8 on one rank) is refused
+    on the host before any launch."""
+    from cmpc.coupled import CoupledRank
+
+    class _Ctx:
+        B = 8
+        cfg = type("cfg", (), {"S": 2, "nV": 4})()
+
+    with pytest.raises(ValueError, match="S_total"):
+        CoupledRank(_Ctx(), 64, 8, 0, 1, None)
