@@ -228,9 +228,13 @@ void cmpc_build_rows_kernel(BuildParams P) {
   // tools/rows_timing.py).  Each wave lowers its issue priority as it
   // completes quarters of its share, so waves that are behind win arbitration.
   const int share = (ngroups + nwaves - 1) / nwaves;
+  // The oldest waves take the groups left over when nwaves does not divide
+  // ngroups (round 3: giving them to the youngest instead, or priority by
+  // quarters of the wave's own share, measured slower)
+  const int g_first = blockIdx.x * WPG + wave;
   int done_groups = 0;
   __builtin_amdgcn_s_setprio(3);
-  for (int g = blockIdx.x * WPG + wave; g < ngroups; g += nwaves) {
+  for (int g = g_first; g < ngroups; g += nwaves) {
     CMPC_T(5)  // loop back-edge / tail of the previous group
 #if CMPC_ROWS_PRIO == 2
     __builtin_amdgcn_s_setprio(3);  // latency-bound prologue first
@@ -564,6 +568,10 @@ void cmpc_build_rows_kernel(BuildParams P) {
     dbg[9] = (double)(t1r - t0r);  // 100 MHz ticks of the same span
     dbg[10] = (double)t0r;
     dbg[11] = (double)t1r;
+    // placement: HW_ID (wave, simd, pipe, cu, sh, se, ...) and XCC_ID
+    dbg[12] = (double)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    dbg[13] = (double)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    dbg[14] = (double)(blockIdx.x * WPG + wave);
   }
 #endif
 }

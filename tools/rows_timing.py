@@ -16,8 +16,13 @@ lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
 with cmpc.Context(cfg, B) as ctx:
     ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
     ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
-    for _ in range(5):
-        ctx.build()
+    import time
+    t_end = time.perf_counter() + 0.3  # settle at the steady clock
+    while time.perf_counter() < t_end:
+        for _ in range(16):
+            ctx.build()
+        ctx.synchronize()
+    ctx.build()
     ctx.synchronize()
     H, f, G = ctx.download_qp()
 raw = np.concatenate([H.reshape(H.shape[0], -1), f, G.reshape(G.shape[0], -1)], axis=1).reshape(-1)
@@ -37,3 +42,34 @@ span = (en.max() - st.min()) / 100e6 * 1e3
 print(f"  kernel span (first wave start -> last wave end): {span:.4f} ms; wave lifetime ms: "
       f"min {d[:, 9].min() / 1e5:.4f} median {np.median(d[:, 9]) / 1e5:.4f} max {d[:, 9].max() / 1e5:.4f}; "
       f"start skew max {(st.max() - st.min()) / 1e5:.4f} ms")
+
+# placement (HW_ID, XCC_ID): per-SIMD group counts against wave end times
+hw = d[:, 12].astype(np.int64)
+xcc = d[:, 13].astype(np.int64) & 0xF
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 0xF
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 7
+key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+simd_key = key * 4 + simd
+t0 = st.min()
+end_us = (en - t0) / 100.0
+print(f"  XCDs {len(np.unique(xcc))}, CUs {len(np.unique(key))}, SIMDs {len(np.unique(simd_key))}")
+grp = {}
+for k_, n_, e_ in zip(simd_key, d[:, 6], end_us):
+    g_ = grp.setdefault(k_, [0, 0, 0.0])
+    g_[0] += n_; g_[1] += 1; g_[2] = max(g_[2], e_)
+tot_g = np.array([v[0] for v in grp.values()]); nw = np.array([v[1] for v in grp.values()])
+last = np.array([v[2] for v in grp.values()])
+for n_ in np.unique(tot_g):
+    m_ = tot_g == n_
+    print(f"  SIMDs with {n_:.0f} groups: {m_.sum():4d} (waves/SIMD {np.unique(nw[m_])}); last wave end "
+          f"us: median {np.median(last[m_]):.1f} max {last[m_].max():.1f}")
+for x_ in np.unique(xcc):
+    m_ = xcc == x_
+    print(f"  XCC {x_}: waves {m_.sum()}, clock median {np.median(clk[m_]):.3f} GHz, wave end us median "
+          f"{np.median(end_us[m_]):.1f} max {end_us[m_].max():.1f}")
+for n_ in np.unique(d[:, 6]):
+    m_ = d[:, 6] == n_
+    print(f"  waves with {n_:.0f} groups: {m_.sum()}, end us median {np.median(end_us[m_]):.1f} "
+          f"max {end_us[m_].max():.1f}")
