@@ -390,13 +390,13 @@ def main():
         try:
             warm()
             for i in range(2):
-                ctx.bind_lin(batches[i % NB].data_ptr())
+                bind(i)
                 ctx.step(1, 0)
             ctx.synchronize()
             reps1 = max(10, args.steps // 2)
             t0 = time.perf_counter()
             for i in range(reps1):
-                ctx.bind_lin(batches[i % NB].data_ptr())
+                bind(i)
                 ctx.step(1, 0)
             ctx.synchronize()
             t_k1 = (time.perf_counter() - t0) / reps1
@@ -404,6 +404,10 @@ def main():
                   "note": "K = 1 Jacobi iteration per step (build-dominated), this rank's GPU"}
         except Exception as e:  # reported, never required
             log(f"K=1 variant failed: {e}")
+        finally:  # the sections below run on the context's own state buffers
+            ctx.bind_state()
+            ctx.bind_lin(0)
+            restore()
 
         # Closed-loop variant (reported beside the metric, not in `value`): the
         # records are produced on the device from plant states each step
