@@ -71,6 +71,12 @@
 #ifndef CMPC_ROWS_FUSE
 #define CMPC_ROWS_FUSE 1  // chain and gather FMAs of a step in one interleaved block
 #endif
+#ifndef CMPC_ROWS_AS0
+#define CMPC_ROWS_AS0 1  // 0: no software-pipelined LDS consumption (PIPE) in any instantiation
+#endif
+#ifndef CMPC_ROWS_SPLIT
+#define CMPC_ROWS_SPLIT 5  // chain link groups before the gather columns' running sums (0: none)
+#endif
 #ifndef CMPC_ROWS_PRIO
 #define CMPC_ROWS_PRIO 1  // 1: priority by progress; 2: + prologue at top priority
 #endif
@@ -109,6 +115,10 @@ void cmpc_build_rows_kernel(BuildParams P) {
   constexpr int NDW = ND > 0 ? ND : 1;
   constexpr int U = CMPC_ROWS_U;   // horizon-loop unroll (immediate LDS offsets)
   static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
+  // software-pipelined LDS consumption (CMPC_ROWS_SPLIT, CMPC_ROWS_AS0; round
+  // 3) where the registers allow it without scratch: the parallel plant's
+  // coop / ncoop kernels with plain lines (the bench kernel among them)
+  constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 && NY <= 3 && NV <= 4 && !RING;
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -428,13 +438,25 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // chain start, rd after the chain), and the scheduling barrier keeps the
 // compiler from sinking them next to their use.
 #if CMPC_ROWS_FUSE && CMPC_RX != 3
-// the running sum of the gather columns first (rd was read a step earlier),
-// then the chain and the gather FMAs in one interleaved block: 4 + nV
-// accumulators in flight (same FMA order per accumulator as two blocks)
+// PIPE (kernels without register headroom excepted): the first
+// CMPC_ROWS_SPLIT link groups of the chain, then the running sums of the
+// gather columns (they consume the LDS reads at the end of the previous step:
+// placed here, the wave does not wait on that round trip at the top of every
+// step), then the other link groups with the gather FMAs interleaved.  The
+// same FMA order per accumulator as the single block.
 #define CMPC_ROWS_CG()                                                      \
-    _Pragma("unroll") for (int o = 0; o < NY; ++o)                          \
-        cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
-    rows_chain_gacc<NS, NY, ND, NUT, NU, M>(pP, pS, mP, mS, aP, aS, cv, acc); \
+    if constexpr (PIPE) {                                                   \
+      rows_chain_head<NS, NY, ND, CMPC_ROWS_SPLIT>(pP, pS, mP, mS, aP, aS); \
+      __builtin_amdgcn_sched_barrier(0);                                    \
+      _Pragma("unroll") for (int o = 0; o < NY; ++o)                        \
+          cv[o] = __builtin_fma(smask, cv[o], rd[o]);                       \
+      __builtin_amdgcn_sched_barrier(0);                                    \
+      rows_chain_gacc_tail<NS, NY, ND, NUT, NU, M, CMPC_ROWS_SPLIT>(pP, pS, mP, mS, aP, aS, cv, acc); \
+    } else {                                                                \
+      _Pragma("unroll") for (int o = 0; o < NY; ++o)                        \
+          cv[o] = __builtin_fma(smask, cv[o], rd[o]);                       \
+      rows_chain_gacc<NS, NY, ND, NUT, NU, M>(pP, pS, mP, mS, aP, aS, cv, acc); \
+    }                                                                       \
     __builtin_amdgcn_sched_barrier(0);
 #else
 #define CMPC_ROWS_CG()                                                      \
@@ -444,9 +466,17 @@ void cmpc_build_rows_kernel(BuildParams P) {
         cv[o] = __builtin_fma(smask, cv[o], rd[o]);                         \
     if (CMPC_RX != 3) rows_gacc<NY, NUT, NU, M>(cv, acc);
 #endif
+// PIPE: the free-response chain's start value base + y_hat of the next step
+// is formed at the end of this step (its y_hat was read at the top of this
+// step), so the first instructions of a step need no LDS value: at the head
+// of an unrolled block the wave no longer waits on the previous block's LDS
+// reads before its first FMA (the same addition, bit-identical)
+#define CMPC_ROWS_AS_BEGIN() double aS = PIPE ? aS0 : base + yh;
+#define CMPC_ROWS_AS_END() \
+  if constexpr (PIPE) aS0 = base + yh;
 #define CMPC_ROWS_STEP(u)                                                   \
   {                                                                         \
-    double aS = base + yh;                                                  \
+    CMPC_ROWS_AS_BEGIN()                                                    \
     yh = yp[u];                                                             \
     double aP[NY];                                                          \
     _Pragma("unroll") for (int o = 0; o < NY; ++o) aP[o] = 0.0;             \
@@ -460,6 +490,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     if (CMPC_RX != 1) {                                                     \
       _Pragma("unroll") for (int o = 0; o < NY; ++o) rd[o] = rq[(u) * NY + o]; \
     }                                                                       \
+    CMPC_ROWS_AS_END()                                                      \
     __builtin_amdgcn_sched_barrier(0);                                      \
   }
 #define CMPC_ROWS_TAIL()                                                    \
@@ -478,6 +509,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
     }
 #endif
     int r = 0;
+    double aS0 = base + yh;  // CMPC_ROWS_AS0: start value of the next step's free-response chain
+    (void)aS0;
     for (int sg = 0; sg <= nseg; ++sg) {
       int r_end = pp;
 #pragma unroll
@@ -525,6 +558,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
     }
 #undef CMPC_ROWS_STEP
 #undef CMPC_ROWS_TAIL
+#undef CMPC_ROWS_AS_BEGIN
+#undef CMPC_ROWS_AS_END
 #undef CMPC_ROWS_CG
 #pragma unroll
     for (int o = 0; o < NY; ++o) cv[o] = __builtin_fma(smask, cv[o], rd[o]);

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Bit-identity of two libcmpc builds' condensed QPs (H, f, G) on the same
+inputs, row build kernel, several configurations (e.g. a scheduling-only
+kernel change).  usage: python tools/compare_build_libs.py LIB_A LIB_B"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = [("par", "coop", 50, 20001), ("par", "coop", 20, 4096), ("par", "coop", 100, 8192),
+         ("par", "ncoop", 50, 8192), ("par", "cent", 50, 8192), ("ser", "coop", 50, 8192)]
+CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import cmpc
+from cmpc.configs import reference_setup
+from cmpc.synthetic import synthetic_batch
+plant, ctype, p, B, out = sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
+cfg = cmpc.reference_config(plant, ctype, p=p)
+arr = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
+lin, u, du, ws = synthetic_batch(cfg, B, seed=31, n_distinct=512)
+with cmpc.Context(cfg, B) as ctx:
+    ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
+    ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
+    ctx.build()
+    H, f, G = ctx.download_qp()
+np.savez(out, H=H, f=f, G=G)
+'''
+bad = 0
+with tempfile.TemporaryDirectory() as td:
+    for plant, ctype, p, B in CASES:
+        res = []
+        for k, lib in enumerate(sys.argv[1:3]):
+            out = os.path.join(td, f"{k}.npz")
+            env = dict(os.environ, CMPC_LIBRARY=os.path.abspath(lib))
+            subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "compressor-mpc_amd"), plant, ctype,
+                            str(p), str(B), out], env=env, check=True, timeout=300)
+            res.append(np.load(out))
+        same = all(np.array_equal(res[0][x], res[1][x]) for x in ("H", "f", "G"))
+        bad += not same
+        print(f"{plant}-{ctype} p={p} B={B}: {'bit-identical' if same else 'DIFFERENT'}", flush=True)
+sys.exit(1 if bad else 0)

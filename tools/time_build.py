@@ -29,7 +29,7 @@ for p in PS:
                 for _ in range(8): ctx.build()
                 ctx.synchronize()
             ctx.enable_timing(True)
-            for _ in range(40): ctx.build()
+            for _ in range(int(os.environ.get("CMPC_TB_N", "40"))): ctx.build()
             ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
             name = "wave" if v == cmpc.CMPC_BUILD_WAVE else "rows"
             print(f"p={p:4d}  {name} build {ms/n:.4f} ms  per QP-step {ms/n*1e6/(B*cfg.S*p):.3f} ns"
