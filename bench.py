@@ -567,17 +567,23 @@ def main():
         # SURVEY config 4 (sub-controllers sharded over the ranks, RCCL all-gather
         # of the plans once per Jacobi iteration), beside the metric: every rank
         # takes part, so at world N it times the exchange over xGMI
-    coupled = None
+    coupled, rc, el_c = None, None, float("inf")
     if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench
-        rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
-                               steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds,
-                               force_collective=bool(dist), tiles=args.coupled_tiles)
-        tc = torch.tensor([rc["elapsed_s"]], dtype=torch.float64,
+        try:  # reported beside the metric, never required for it
+            rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
+                                   steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds,
+                                   force_collective=bool(dist), tiles=args.coupled_tiles)
+        except Exception as e:
+            log(f"[rank {rank}] coupled section failed: {e}")
+        # every rank joins the reduction; a failed rank reports +inf, so the
+        # section is dropped everywhere
+        tc = torch.tensor([rc["elapsed_s"] if rc else float("inf")], dtype=torch.float64,
                           device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
         if dist:
             dist.all_reduce(tc, op=dist.ReduceOp.MAX)
         el_c = float(tc.item())
+    if rc and el_c != float("inf"):
         coupled = dict(rc)
         coupled.pop("elapsed_s")
         coupled.update({
