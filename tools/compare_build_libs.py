@@ -11,7 +11,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [("par", "coop", 50, 20001), ("par", "coop", 20, 4096), ("par", "coop", 100, 8192),
-         ("par", "ncoop", 50, 8192), ("par", "cent", 50, 8192), ("ser", "coop", 50, 8192)]
+         ("par", "ncoop", 50, 8192), ("par", "cent", 50, 8192), ("ser", "coop", 50, 8192),
+         ("ser", "coop", 100, 8192), ("ser", "cent", 100, 8192), ("par", "cent", 200, 4096)]
 CHILD = r'''
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1])
