@@ -74,9 +74,6 @@
 #ifndef CMPC_ROWS_AS0
 #define CMPC_ROWS_AS0 1  // 0: no software-pipelined LDS consumption (PIPE) in any instantiation
 #endif
-#ifndef CMPC_ROWS_PIPE_WPE2
-#define CMPC_ROWS_PIPE_WPE2 1  // PIPE also in the 256-register (WPE = 2) instantiations (round 3: serial p = 100 -1.2 %)
-#endif
 #ifndef CMPC_ROWS_SPLIT
 #define CMPC_ROWS_SPLIT 5  // chain link groups before the gather columns' running sums (0: none)
 #endif
@@ -120,11 +117,8 @@ void cmpc_build_rows_kernel(BuildParams P) {
   static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
   // software-pipelined LDS consumption (CMPC_ROWS_SPLIT, CMPC_ROWS_AS0; round
   // 3) where the registers allow it without scratch: the parallel plant's
-  // coop / ncoop kernels with plain lines (the bench kernel among them), and
-  // every 256-register (WPE = 2) instantiation (153-191 VGPRs, no scratch;
-  // H/f/G bit-identical, profiles/r3_pipe_wpe2_ab.txt)
-  constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 &&
-                        ((NY <= 3 && NV <= 4 && !RING) || (CMPC_ROWS_PIPE_WPE2 && WPE == 2));
+  // coop / ncoop kernels with plain lines (the bench kernel among them)
+  constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 && NY <= 3 && NV <= 4 && !RING;
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
