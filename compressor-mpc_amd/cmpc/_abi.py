@@ -91,7 +91,7 @@ EXPORTS = (
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
     "cmpc_bind_state",
-    "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate",
+    "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate", "cmpc_coupled_validate",
     "cmpc_get_input", "cmpc_get_input_host", "cmpc_update_u", "cmpc_update_u_host",
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
@@ -205,8 +205,10 @@ def load_library(path: str = LIB_PATH):
         "cmpc_get_input_host": ([c_void, P(dbl), u32], ctypes.c_int),
         "cmpc_update_u": ([c_void, c_void], ctypes.c_int),
         "cmpc_update_u_host": ([c_void, P(dbl)], ctypes.c_int),
-        "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, c_void,
-                                  c_void, u32], ctypes.c_int),
+        "cmpc_coupled_validate": ([P(CmpcDims), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                   ctypes.c_size_t], ctypes.c_int),
+        "cmpc_coupled_iterate": ([c_void, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void, ctypes.c_size_t,
+                                  c_void, ctypes.c_size_t, c_void, u32], ctypes.c_int),
         "cmpc_qp_solve_batch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(dbl),
                                  P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32), ctypes.c_int,
                                  P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],

@@ -99,32 +99,56 @@ class CoupledRank:
         nV = ctx.cfg.nV
         dev = G_ext.device
         self.G_ext = G_ext
-        self.du_local = torch.zeros(nqp, nV, dtype=torch.float64, device=dev)
-        self.du_all = torch.zeros(world, nqp, nV, dtype=torch.float64, device=dev)
+        # world size 1 without the collective: the plans ping-pong between two
+        # buffers (an iteration reads the one the previous iteration wrote and
+        # writes the other), so no gather copy is needed.  A kernel may not
+        # read and write the same plan buffer: its waves run side by side.
+        self.local_only = world == 1 and not force_collective
+        self._plans = [torch.zeros(nqp, nV, dtype=torch.float64, device=dev)
+                       for _ in range(2 if self.local_only else 1)]
+        self._cur = 0  # the buffer holding the current plans
+        self._all = (None if self.local_only else
+                     torch.zeros(world, nqp, nV, dtype=torch.float64, device=dev))
         # one stream for the library and torch's collectives
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
 
+    @property
+    def du_local(self):
+        """This rank's current plans [nqp][nV] (the next gather's input)."""
+        return self._plans[self._cur]
+
+    @property
+    def du_all(self):
+        """The gathered plans [world][nqp][nV] the next iteration reads."""
+        if self.local_only:
+            return self._plans[self._cur].view(1, *self._plans[self._cur].shape)
+        return self._all
+
     def gather(self):
         import torch.distributed as dist
-        if self.world == 1 and not self.force_collective:
-            self.du_all[0].copy_(self.du_local)
+        if self.local_only:  # the current plans are the gathered ones
             return
         if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(self.du_all, self.du_local, group=self.group)
+            dist.all_gather_into_tensor(self._all, self.du_local, group=self.group)
         else:  # gloo: CPU staging
             parts = [self.torch.zeros_like(self.du_local, device="cpu") for _ in range(self.world)]
             dist.all_gather(parts, self.du_local.cpu(), group=self.group)
-            self.du_all.copy_(self.torch.stack(parts))
+            self._all.copy_(self.torch.stack(parts))
 
     def iterate(self, apply_move: bool):
         from . import CMPC_APPLY_MOVE
         from ._abi import check
         lib = self.ctx.lib
+        src = self.du_all
+        nxt = 1 - self._cur if self.local_only else self._cur
+        out = self._plans[nxt]
         check(lib.cmpc_coupled_iterate(
             self.ctx._h, self.S_total, self.S_local, self.s_offset,
-            ctypes.c_void_p(self.G_ext.data_ptr()), ctypes.c_void_p(self.du_all.data_ptr()),
-            ctypes.c_void_p(self.du_local.data_ptr()), CMPC_APPLY_MOVE if apply_move else 0),
+            ctypes.c_void_p(self.G_ext.data_ptr()), self.G_ext.numel(),
+            ctypes.c_void_p(src.data_ptr()), src.numel(),
+            ctypes.c_void_p(out.data_ptr()), CMPC_APPLY_MOVE if apply_move else 0),
             "cmpc_coupled_iterate")
+        self._cur = nxt
 
     def step(self, K: int):
         """build + K gathered Jacobi iterations (the first move applied)."""
@@ -192,6 +216,8 @@ def make_coupled_tiles(cfg, arr, lin, u_old, S_total: int, S_local: int, rank: i
             ctx.init_warmstart()
             _, _, G = ctx.download_qp()
             G_ext = torch.from_numpy(synthetic_g_ext(G, S_total, S_local, rank * S_local, t * bt)).to(dev)
+            # the copy ran on the current stream; the tile's stream reads G_ext
+            s.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(s):
                 out.append(CoupledRank(ctx, S_total, S_local, rank, world, G_ext, group=group,
                                        force_collective=force_collective))
@@ -230,9 +256,28 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
     cfg = reference_config("par", "coop", p=p)
     arr = controller_arrays(cfg, reference_setup("par", "coop"))
     nqp = B * S_local
-    lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=500 + rank, n_distinct=1024)
-    crs, streams = make_coupled_tiles(cfg, arr, lin, u_old, S_total, S_local, rank, world, device,
-                                      tiles, group=group, force_collective=force_collective)
+    collective = world > 1 or force_collective
+    crs, streams, err = [], [], None
+    try:
+        lin, u_old, _, _ = synthetic_batch(cfg, nqp // cfg.S, seed=500 + rank, n_distinct=1024)
+        crs, streams = make_coupled_tiles(cfg, arr, lin, u_old, S_total, S_local, rank, world, device,
+                                          tiles, group=group, force_collective=force_collective)
+    except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised
+        err = e
+    if collective:
+        # every rank agrees that its set-up succeeded before the first
+        # collective of the timed section: a rank that failed alone would
+        # otherwise leave its peers waiting in (or mis-pairing) the gathers
+        on_gpu = dist.get_backend(group) == "nccl"
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32,
+                          device=f"cuda:{device}" if on_gpu else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) == 0 and err is None:
+            err = RuntimeError("coupled section: set-up failed on another rank")
+    if err is not None:
+        for c in crs:
+            c.ctx.close()
+        raise err
     try:
         cr = CoupledPipeline(crs, streams)
         for _ in range(warmup):

@@ -1565,14 +1565,39 @@ int cmpc_update_u_host(cmpc_ctx* c, const double* du_full) {
   return cmpc_update_u(c, d[0]);
 }
 
+int cmpc_coupled_validate(const cmpc_dims* d, int S_total, int S_local, int s_offset, size_t G_ext_len,
+                          size_t du_all_len) {
+  if (!d) return fail("cmpc_coupled_validate: null dims");
+  cmpc_layout L;
+  if (layout_of(d, &L)) return -1;
+  const long long nqp_ll = (long long)d->B * d->S;
+  if (S_local < 1 || nqp_ll % S_local || S_local % d->S)
+    return fail("cmpc_coupled_iterate: S_local must divide B*S and be a multiple of S");
+  if (S_total < S_local || S_total % S_local || s_offset < 0 || s_offset % S_local ||
+      s_offset + S_local > S_total)
+    return fail("cmpc_coupled_iterate: bad S_total / s_offset");
+  // every read of the kernel must fall inside the caller's buffers: G_ext
+  // holds nV x (S_total-1) nV per local QP, du_all the plans of all S_total
+  // sub-controllers of the B scenarios (rank-major, S_total / S_local ranks)
+  const size_t nV = (size_t)L.nV, nqp = (size_t)nqp_ll, B = nqp / (size_t)S_local;
+  const size_t need_g = nV * (size_t)(S_total - 1) * nV * nqp;
+  const size_t need_d = (size_t)S_total * B * nV;
+  if (G_ext_len < need_g)
+    return fail("cmpc_coupled_iterate: G_ext holds " + std::to_string(G_ext_len) + " doubles, the kernel reads " +
+                std::to_string(need_g) + " (nV*(S_total-1)*nV per local QP)");
+  if (du_all_len < need_d)
+    return fail("cmpc_coupled_iterate: du_all holds " + std::to_string(du_all_len) + " doubles, the kernel reads " +
+                std::to_string(need_d) + " (S_total x B x nV: every rank's plans; does S_local x world cover "
+                "S_total?)");
+  return 0;
+}
+
 int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, const double* G_ext,
-                         const double* du_all, double* du_out, uint32_t flags) {
+                         size_t G_ext_len, const double* du_all, size_t du_all_len, double* du_out,
+                         uint32_t flags) {
   if (!c) return fail("null context");
   if (!G_ext || !du_all) return fail("cmpc_coupled_iterate: null argument");
-  if (S_local < 1 || c->nqp % S_local || S_local % c->d.S)
-    return fail("cmpc_coupled_iterate: S_local must divide B*S and be a multiple of S");
-  if (S_total < S_local || S_total % S_local || s_offset % S_local || s_offset + S_local > S_total)
-    return fail("cmpc_coupled_iterate: bad S_total / s_offset");
+  if (cmpc_coupled_validate(&c->d, S_total, S_local, s_offset, G_ext_len, du_all_len)) return -1;
   if (ensure_cfg(c)) return -1;
   HIP_TRY(hipSetDevice(c->device));
   CoupledParams P;

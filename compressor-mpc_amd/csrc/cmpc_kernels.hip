@@ -57,6 +57,19 @@
 #else
 #define CMPC_EXP_YH(...) __VA_ARGS__
 #endif
+#ifndef CMPC_BUILD_ILP
+#define CMPC_BUILD_ILP 1
+#endif
+#if CMPC_BUILD_ILP == 4
+#define CMPC_ILP_PROP(pv, m, ax) prop4w_dpp<NS, ND>(pv, m, ax)
+#define CMPC_ILP_SUM(ax) (((ax)[0] + (ax)[1]) + ((ax)[2] + (ax)[3]))
+#elif CMPC_BUILD_ILP == 3
+#define CMPC_ILP_PROP(pv, m, ax) prop3w_dpp<NS, ND>(pv, m, ax)
+#define CMPC_ILP_SUM(ax) (((ax)[0] + (ax)[1]) + (ax)[2])
+#elif CMPC_BUILD_ILP == 2
+#define CMPC_ILP_PROP(pv, m, ax) prop2w_dpp<NS, ND>(pv, m, (ax)[0], (ax)[1])
+#define CMPC_ILP_SUM(ax) ((ax)[0] + (ax)[1])
+#endif
 #if CMPC_EXP == 5
 #define CMPC_EXP_STEP(pv, m, a, va, acc)                  \
   {                                                       \
@@ -67,6 +80,20 @@
   }
 #elif CMPC_EXP == 6
 #define CMPC_EXP_STEP(pv, m, a, va, acc) prop1w_gacc_dpp<NS, ND, NUT, NU, M>(pv, m, a, va, acc)
+#elif CMPC_BUILD_ILP > 1
+// several partial accumulators per chain (small batches: one wave per SIMD
+// has no other wave to hide the dependent FP64 latency); the gather column
+// update runs after the chain, off its critical path
+#define CMPC_EXP_STEP(pv, m, a, va, acc)                                   \
+  {                                                                        \
+    double ax_[CMPC_BUILD_ILP];                                            \
+    ax_[0] = a;                                                            \
+    for (int k_ = 1; k_ < CMPC_BUILD_ILP; ++k_) ax_[k_] = 0.0;             \
+    CMPC_ILP_PROP(pv, m, ax_);                                             \
+    a = CMPC_ILP_SUM(ax_);                                                 \
+    va = __builtin_fma(smask, va, rd);                                     \
+    CMPC_EXP_GACC(va, acc);                                                \
+  }
 #else
 #define CMPC_EXP_STEP(pv, m, a, va, acc) \
   {                                      \
@@ -388,7 +415,7 @@ void cmpc_build_kernel(BuildParams P) {
     /* chain init: f (states), kappa - yhat_r (outputs), w_{r+2} (carriers) */         \
     double a = __builtin_fma(-ym, yh, base);                                           \
     /* accumulate row r-1: acc[a] += column_a * own column (gather lanes) */          \
-    va = __builtin_fma(smask, va, rd);                                                 \
+    if constexpr (CMPC_BUILD_ILP == 1) va = __builtin_fma(smask, va, rd);              \
     CMPC_EXP_STEP(pv, m, a, va, acc);                                                  \
     CMPC_EXP_YH(if constexpr (!PRE) yh = ylp[(u) * NY]);                               \
     /* a: P rows -> P_{r+1} / raw Markov of step r; sim lanes -> x_{r+2} / z_r */      \

@@ -13,6 +13,7 @@ The DPP sources of a block are never written inside it.
   accum_dpp<LB, NU, M>(v, acc): acc[a][k] += bcast_{LB + a%NU}(v[a/NU]) * v[k]
                                  for a < NU*M, k < M
   prop1w_dpp<NS, ND>(p, m, a): prop1 over lanes 0..NS-1, then lanes 16-ND..15 with m[NS..]
+  prop{3,4}w_dpp<NS, ND>(p, m, a[]): prop1w with link i into a[i % n] (n chains)
   gacc_dpp<NUT, NU, M>(v, acc): acc[a] += bcast_{(a/NU)*NUT + a%NU}(v) * v, a < NU*M
                                  (gather layout: lane k*NUT + c holds QP column (move k, input c))
 """
@@ -102,6 +103,22 @@ def prop2w(ns, nd):
             f"  asm({body}\n      : \"+v\"(a0), \"+v\"(a1)\n      : {ins});\n}}\n")
 
 
+def propnw(ns, nd, na):
+    """na accumulator chains (link i into a_{i mod na}): a dependent chain of
+    about (ns + nd) / na links, for waves that have no other wave on their
+    SIMD to hide the FP64 latency (small batches)"""
+    links = [(l, f"{l}") for l in range(ns)] + [(ns + k, f"{16 - nd + k}") for k in range(nd)]
+    lines = ['"s_nop 1\\n\\t"']
+    for i, (mi, lane) in enumerate(links):
+        lines.append(f'"v_fmac_f64_dpp %{i % na}, %{na}, %{na + 1 + mi} row_newbcast:{lane} {CTRL}\\n\\t"')
+    outs = ", ".join(f'"+v"(a[{k}])' for k in range(na))
+    ins = ", ".join(['"v"(p)'] + [f'"v"(m[{l}])' for l in range(ns + nd)])
+    body = "\n      ".join(lines)
+    return (f"template <> __device__ __forceinline__ void prop{na}w_dpp<{ns}, {nd}>(double p, const double* m,"
+            f" double* a) {{\n"
+            f"  asm({body}\n      : {outs}\n      : {ins});\n}}\n")
+
+
 def accum(lb, nu, mm):
     """acc is double[NU*M][M] flattened as acc[a*M + k]."""
     nv = nu * mm
@@ -164,6 +181,10 @@ def main():
              " double&);\n",
              "template <int NS, int ND> __device__ __forceinline__ void prop2w_dpp(double, const double*,"
              " double&, double&);\n",
+             "template <int NS, int ND> __device__ __forceinline__ void prop3w_dpp(double, const double*,"
+             " double*);\n",
+             "template <int NS, int ND> __device__ __forceinline__ void prop4w_dpp(double, const double*,"
+             " double*);\n",
              "template <int NS, int ND, int NUT, int NU, int M> __device__ __forceinline__ void "
              "prop1w_gacc_dpp(double, const double*, double&, double, double*);\n"]
     for ns in range(2, 16):
@@ -173,6 +194,8 @@ def main():
             if ns + nd <= 16:
                 parts.append(prop1w(ns, nd))
                 parts.append(prop2w(ns, nd))
+                parts.append(propnw(ns, nd, 3))
+                parts.append(propnw(ns, nd, 4))
     # LB = NS (first Markov lane): the instantiated plants have NS = 10, 11
     for lb in (10, 11):
         for nu in (1, 2, 4):

@@ -263,15 +263,25 @@ int cmpc_update_u_host(cmpc_ctx* ctx, const double* du_full);
  * G_ext: device, [nV * (S_total-1) * nV][B*S_local] (element-major),
  *        column block j = the j-th other sub-controller in global order.
  * du_all: device, all-gathered plans [world][B][S_local][nV] (rank-major),
- *        world = S_total / S_local: the kernel reads all of it, so the
- *        caller's buffer must hold S_total * B * nV doubles.
+ *        world = S_total / S_local: the kernel reads all of it.
+ * G_ext_len, du_all_len: the element counts (doubles) of the caller's two
+ *        buffers.  The call is refused (-1, cmpc_last_error) unless
+ *        G_ext_len >= nV*(S_total-1)*nV * B*S_local and
+ *        du_all_len >= S_total * B * nV, i.e. unless every read of the
+ *        kernel falls inside them (a rank layout that does not cover
+ *        S_total would otherwise read past the gathered plans).
  * du_out: device [B*S_local][nV] or NULL: this rank's new plans (the next
  *        all-gather's input).  CMPC_APPLY_MOVE on the last iteration of a
  *        step applies the first move (UpdateUOld) and stores du_old.
  * The caller all-gathers between calls (RCCL; cmpc/coupled.py). */
+/* The checks cmpc_coupled_iterate makes before any launch, for a context of
+ * these dims (B scenarios x S = B*S local QPs): 0, or -1 with
+ * cmpc_last_error().  Host only, no device needed. */
+int cmpc_coupled_validate(const cmpc_dims* dims, int S_total, int S_local, int s_offset,
+                          size_t G_ext_len, size_t du_all_len);
 int cmpc_coupled_iterate(cmpc_ctx* ctx, int S_total, int S_local, int s_offset,
-                         const double* G_ext, const double* du_all, double* du_out,
-                         uint32_t flags);
+                         const double* G_ext, size_t G_ext_len, const double* du_all,
+                         size_t du_all_len, double* du_out, uint32_t flags);
 
 /* Observer and receding-horizon update on the device (SURVEY.md §8(f)
  * row 2).  Each QP slot keeps the state of its sub-controller's

@@ -18,6 +18,12 @@
 //   NerveCenter::GetNextInputWithTiming(y, n, t)      include/nerve_center.h:134-182
 //   InputConstraints<nu> (per sub-controller ctor arg) include/input_constraints.h:12-26
 //   read_files.h setup-file reader                    include/read_files.h:13-81
+//   MpcQpSolver::{SetWeights, GenerateQP, SolveQP, InitializeQPProblem,
+//     SetOutputReference, GetOutputReference}          include/mpc_qp_solver.h:53-97
+//   DistributedSolver::{UpdateAndSolveQP, GenerateDistributedQP}
+//                                                       include/distributed_solver.h:69-94
+//   ParallelCompressors(p_in, p_out), Ts              include/parallel_compressors.h:44-55,
+//                                                       include/common-variables.h (sampling time)
 //
 // Two ways to run a step:
 //  - with the observer (the reference's own pattern): SetObserver(s, M) for
@@ -75,6 +81,11 @@ struct ControllerSpec {
   std::vector<std::vector<int>> input_order;            // ControlInputIndices per sub-controller
   std::vector<std::vector<int>> out_idx;                // ControlledOutputIndices per sub-controller
   std::vector<int> plant_input_index;                   // ControlInputIndex (GetPlantInput)
+  // plant parameters of the linearisation: suction / discharge pressure
+  // (ParallelCompressors(p_in, p_out), parallel_compressors.h:44-55; the
+  // serial plant's SerialCompressors(p_in, p_out), serial_compressors.h) and
+  // the sampling time of the discretisation (common-variables.h: 0.05 s)
+  double p_in = 1.0, p_out = 1.0, Ts = 0.05;
 
   int S() const { return static_cast<int>(input_order.size()); }
   int nV() const { return m * nu; }
@@ -214,6 +225,234 @@ inline cmpc_dims SubControllerDims(const ControllerSpec& spec, int s, int S, int
   return d;
 }
 
+// MpcQpSolver<...>::QP (include/mpc_qp_solver.h:45-50): H (nV x nV,
+// row-major as the reference's RowMajor H) and f; plus, for a reduced
+// (distributed) sub-controller, G = Su' W Su_other (nV x nVo, row-major), the
+// factor ApplyOtherInput multiplies the other controllers' plans with
+// (distributed_solver.h:98-103: f += (du_other' Su_other') y_pred_weight_).
+// This build forms G in the condensation kernel, never Su_other itself.
+struct QP {
+  std::vector<double> H, f, G;
+};
+
+// MpcQpSolver<n_total_states, n_outputs, n_control_inputs, p, m>
+// (include/mpc_qp_solver.h:21-139, libs/mpc_qp_solver.cc) for sub-controller
+// s of spec: its own one-slot device context builds the QP (GenerateQP) and
+// its qpOASES SQProblem's role -- the working set a hotstart starts from --
+// is kept here between SolveQP calls.  SolveQP runs the product's solver
+// (cmpc_qp_solve_batch: the dual active-set method of DESIGN.md §4, nWSR cap
+// 10, zero move on any failure, as libs/mpc_qp_solver.cc:42-75), so for the
+// same QP, u_old and warm start it returns what the batched iterate kernel
+// does, bit for bit.
+//
+// GenerateQP takes what this library condenses from instead of the reference's
+// Prediction (Su, Sx, Sf, never formed here): the sub-controller's lin record
+// (cmpc_layout: the discrete linearisation, the observer's augmented state,
+// y_prev) and the linearisation input u_old (AdjustAllDelayedStates), or the
+// plant state and input, linearised on the host (cmpc_plant_lin_record).
+class MpcQpSolver {
+ public:
+  MpcQpSolver(const ControllerSpec& spec, int s, InputConstraints u_constraints,
+              const std::vector<double>& y_ref = {}, const std::vector<double>& u_weight = {},
+              const std::vector<double>& y_weight = {}, int device = 0)
+      : spec_(spec), s_(s), device_(device), c_(std::move(u_constraints)) {
+    if (s < 0 || s >= spec.S()) throw Error("MpcQpSolver: bad sub-controller index");
+    for (const auto* v : {&c_.lower_bound, &c_.upper_bound, &c_.lower_rate_bound, &c_.upper_rate_bound})
+      if (static_cast<int>(v->size()) != spec.nu) throw Error("InputConstraints: nu values per bound");
+    d_ = SubControllerDims(spec, s, 1, 1);
+    Check(cmpc_create(&ctx_, &d_, device), "cmpc_create");
+    Check(cmpc_get_layout(ctx_, &L_), "cmpc_get_layout");
+    Check(cmpc_set_constraints(ctx_, 0, c_.lower_bound.data(), c_.upper_bound.data(), c_.lower_rate_bound.data(),
+                               c_.upper_rate_bound.data()),
+          "cmpc_set_constraints");
+    // the reference's defaults: y_ref = 0, identity weights (mpc_qp_solver.h:53-57)
+    y_ref_ = y_ref.empty() ? std::vector<double>(static_cast<size_t>(spec.p) * spec.ny, 0.0) : y_ref;
+    std::vector<double> uw = u_weight, yw = y_weight;
+    if (uw.empty()) uw = Identity(spec.nu);
+    if (yw.empty()) yw = Identity(spec.ny);
+    SetWeights(uw.data(), yw.data());
+    SetOutputReference(y_ref_.data());
+  }
+  virtual ~MpcQpSolver() {
+    if (ctx_) cmpc_destroy(ctx_);
+  }
+  MpcQpSolver(const MpcQpSolver&) = delete;
+  MpcQpSolver& operator=(const MpcQpSolver&) = delete;
+  MpcQpSolver(MpcQpSolver&& o) noexcept { *this = std::move(o); }
+  MpcQpSolver& operator=(MpcQpSolver&& o) noexcept {
+    if (this != &o) {
+      if (ctx_) cmpc_destroy(ctx_);
+      spec_ = std::move(o.spec_);
+      s_ = o.s_;
+      device_ = o.device_;
+      c_ = std::move(o.c_);
+      d_ = o.d_;
+      L_ = o.L_;
+      ctx_ = o.ctx_;
+      o.ctx_ = nullptr;
+      y_ref_ = std::move(o.y_ref_);
+      ws_ = o.ws_;
+      status_ = o.status_;
+      nchg_ = o.nchg_;
+    }
+    return *this;
+  }
+
+  /// SetWeights(uwt, ywt) (mpc_qp_solver.h:62-80): uwt nu x nu, ywt ny x ny,
+  /// row-major (W = blkdiag_p(ywt), R = blkdiag_m(uwt)).
+  void SetWeights(const double* uwt, const double* ywt) { Check(cmpc_set_weights(ctx_, 0, uwt, ywt), "cmpc_set_weights"); }
+  /// SetOutputReference(y_ref) (:89): p x ny, prediction-major.
+  void SetOutputReference(const double* y_ref) {
+    y_ref_.assign(y_ref, y_ref + static_cast<size_t>(spec_.p) * spec_.ny);
+    Check(cmpc_set_reference(ctx_, 0, y_ref), "cmpc_set_reference");
+  }
+  /// GetOutputReference() (:92).
+  std::vector<double> GetOutputReference() const { return y_ref_; }
+
+  /// GenerateQP (mpc_qp_solver.h:83-87 / libs/mpc_qp_solver.cc:16-40) from
+  /// the sub-controller's lin record (cmpc_layout().rec_len doubles) and its
+  /// linearisation input u_old (nu_tot, this controller's input order).
+  QP GenerateQP(const double* lin_record, const double* u_old) {
+    const std::vector<double> du(L_.nV, 0.0);
+    const uint32_t ws = 0;
+    Check(cmpc_set_state(ctx_, u_old, du.data(), &ws), "cmpc_set_state");
+    Check(cmpc_upload_lin(ctx_, lin_record), "cmpc_upload_lin");
+    Check(cmpc_build(ctx_), "cmpc_build");
+    QP qp;
+    qp.H.resize(static_cast<size_t>(L_.nV) * L_.nV);
+    qp.f.resize(L_.nV);
+    qp.G.resize(static_cast<size_t>(L_.nV) * L_.nVo);
+    Check(cmpc_download_qp(ctx_, qp.H.data(), qp.f.data(), L_.nVo ? qp.G.data() : nullptr), "cmpc_download_qp");
+    return qp;
+  }
+  /// GenerateQP at a plant state: x (ns), u_full (the plant's n_inputs), the
+  /// observer's augmented-state tail dx_aug (naug, null = 0), y_prev
+  /// (n_outputs), u_old (nu_tot, this controller's order).  The
+  /// linearisation and discretisation run on the host (the reference's
+  /// AugmentedLinearizedSystem::Update, aug_lin_sys.cc:145-177).
+  QP GenerateQP(const double* x, const double* u_full, const double* dx_aug, const double* y_prev,
+                const double* u_old) {
+    std::vector<double> rec(L_.rec_len, 0.0);
+    Check(cmpc_plant_lin_record(static_cast<int>(spec_.plant), spec_.p_in, spec_.p_out, spec_.Ts, x, u_full,
+                                spec_.input_order[s_].data(), spec_.out_idx[s_].data(), &d_, rec.data()),
+          "cmpc_plant_lin_record");
+    for (int i = 0; i < L_.naug; ++i) rec[L_.off_x + i] = dx_aug ? dx_aug[i] : 0.0;
+    for (int o = 0; o < spec_.ny; ++o) rec[L_.off_y + o] = y_prev[spec_.out_idx[s_][o]];
+    return GenerateQP(rec.data(), u_old);
+  }
+
+  /// InitializeQPProblem(qp, u_old) (libs/mpc_qp_solver.cc:77-101): a cold
+  /// solve whose working set the next hotstart starts from; its status is
+  /// ignored, as the reference's.
+  void InitializeQPProblem(const QP& qp, const double* u_old) {
+    std::vector<double> x(L_.nV);
+    Solve(qp, qp.f.data(), u_old, 0u, x.data());
+  }
+  /// SolveQP(qp, u_old) (libs/mpc_qp_solver.cc:42-75): hotstart from the
+  /// last solve's working set, nWSR <= 10; the zero vector on any failure.
+  /// u_old: this controller's own inputs (nu).
+  std::vector<double> SolveQP(const QP& qp, const double* u_old) {
+    std::vector<double> x(L_.nV);
+    Solve(qp, qp.f.data(), u_old, ws_, x.data());
+    return x;
+  }
+  /// Solver status word (CMPC_QP_*) and working-set changes of the last solve.
+  int last_status() const { return status_; }
+  int last_nwsr() const { return nchg_; }
+  /// the working-set word the next hotstart starts from
+  uint32_t working_set() const { return ws_; }
+  const cmpc_layout& layout() const { return L_; }
+  cmpc_ctx* handle() { return ctx_; }
+
+ protected:
+  void Solve(const QP& qp, const double* f, const double* u_old, uint32_t ws_in, double* x) {
+    const int nV = L_.nV, nu = spec_.nu;
+    if (static_cast<int>(qp.H.size()) != nV * nV || static_cast<int>(qp.f.size()) != nV)
+      throw Error("MpcQpSolver::SolveQP: QP of another size");
+    // lb = rep_m(lower - u_old), ub = rep_m(upper - u_old), lbA/ubA = rep_m(rate)
+    std::vector<double> lb(nV), ub(nV), lbA(nV), ubA(nV);
+    for (int i = 0; i < nV; ++i) {
+      lb[i] = c_.lower_bound[i % nu] - u_old[i % nu];
+      ub[i] = c_.upper_bound[i % nu] - u_old[i % nu];
+      lbA[i] = c_.lower_rate_bound[i % nu];
+      ubA[i] = c_.upper_rate_bound[i % nu];
+    }
+    int32_t status = 0, nchg = 0, ntrace = 0;
+    uint32_t ws_out = 0;
+    uint8_t trace[16];
+    Check(cmpc_qp_solve_batch(device_, nV, nu, 1, qp.H.data(), f, lb.data(), ub.data(), lbA.data(), ubA.data(),
+                              &ws_in, CMPC_NWSR_MAX, x, &status, &nchg, &ws_out, trace, &ntrace),
+          "cmpc_qp_solve_batch");
+    ws_ = ws_out;
+    status_ = status;
+    nchg_ = nchg;
+  }
+  static std::vector<double> Identity(int n) {
+    std::vector<double> I(static_cast<size_t>(n) * n, 0.0);
+    for (int i = 0; i < n; ++i) I[i * n + i] = 1.0;
+    return I;
+  }
+
+  ControllerSpec spec_;
+  int s_ = 0, device_ = 0;
+  InputConstraints c_;
+  cmpc_dims d_{};
+  cmpc_layout L_{};
+  cmpc_ctx* ctx_ = nullptr;
+  std::vector<double> y_ref_;
+  uint32_t ws_ = 0;
+  int status_ = 0, nchg_ = 0;
+};
+
+// DistributedSolver<...> (include/distributed_solver.h:12-123): MpcQpSolver
+// plus the update of a QP by the other sub-controllers' plans.
+class DistributedSolver : public MpcQpSolver {
+ public:
+  /// DistributedSolver(index, u_constraints, y_ref, u_weight, y_weight)
+  /// (distributed_solver.h:57-64); index = the sub-controller s of spec.
+  DistributedSolver(const ControllerSpec& spec, int index, InputConstraints u_constraints,
+                    const std::vector<double>& y_ref = {}, const std::vector<double>& u_weight = {},
+                    const std::vector<double>& y_weight = {}, int device = 0)
+      : MpcQpSolver(spec, index, std::move(u_constraints), y_ref, u_weight, y_weight, device) {}
+
+  /// GenerateDistributedQP(qp, ...) (:83-94): the step's QP incl. G.
+  void GenerateDistributedQP(QP* qp, const double* lin_record, const double* u_old) {
+    *qp = GenerateQP(lin_record, u_old);
+  }
+  /// UpdateAndSolveQP(qp, du_out, u_old, Su_other, du_other) (:69-80):
+  /// ApplyOtherInput on *qp (f += G du_other; the caller passes a copy of
+  /// the step's QP, as distributed_controller.h:214 does), then SolveQP.
+  /// du_other: the other controllers' plans, controller-major, then move,
+  /// then input (nerve_center.h:283-285), m * (nu_tot - nu) values.
+  void UpdateAndSolveQP(QP* qp, std::vector<double>* du_out, const double* u_old, const double* du_other) {
+    ApplyOtherInput(qp, du_other);
+    *du_out = SolveQP(*qp, u_old);
+  }
+
+ private:
+  // f_k[a] = f[a] + sum_c G[a][c] du[c], c ascending over G's columns (move,
+  // then other input), each product rounded before the add: the order and
+  // rounding of the iterate kernel (cmpc_kernels.hip, f_k = f + G du_other)
+  void ApplyOtherInput(QP* qp, const double* du_other) {
+    const int nV = L_.nV, nVo = L_.nVo, nu = spec_.nu;
+    if (!nVo) return;
+    if (static_cast<int>(qp->G.size()) != nV * nVo) throw Error("UpdateAndSolveQP: QP without G");
+    const int sm1 = nVo / nV, m = spec_.m;
+    std::vector<double> d(nVo);
+    for (int rk = 0; rk < sm1; ++rk)
+      for (int mv = 0; mv < m; ++mv)
+        for (int c = 0; c < nu; ++c) d[mv * (sm1 * nu) + rk * nu + c] = du_other[rk * nV + mv * nu + c];
+    for (int a = 0; a < nV; ++a) {
+      double t = qp->f[a];
+      for (int c = 0; c < nVo; ++c) {
+        volatile double prod = qp->G[a * nVo + c] * d[c];  // no contraction into an FMA
+        t = t + prod;
+      }
+      qp->f[a] = t;
+    }
+  }
+};
+
 // DistributedController<AugLinSys, ...>(sys, constraints, M)
 // (include/distributed_controller.h:126-128).  Two uses, as in the reference:
 //  - the constructor arguments of one sub-controller of a NerveCenter
@@ -233,7 +472,7 @@ class DistributedController {
       : constraints_(std::move(constraints)), M_(std::move(M)) {}
   DistributedController(const ControllerSpec& spec, int s, InputConstraints constraints,
                         std::vector<double> M, int device = 0)
-      : constraints_(std::move(constraints)), M_(std::move(M)), dev_(std::make_shared<Device>()) {
+      : constraints_(std::move(constraints)), M_(std::move(M)), dev_(std::make_unique<Device>()) {
     if (s < 0 || s >= spec.S()) throw Error("DistributedController: bad sub-controller index");
     if (static_cast<int>(M_.size()) != (spec.ns + spec.ndist) * spec.n_outputs)
       throw Error("DistributedController: M must be (ns + ndist) x n_outputs");
@@ -250,6 +489,23 @@ class DistributedController {
           "cmpc_set_constraints");
     Check(cmpc_set_observer(dev_->ctx, 0, spec.n_outputs, M_.data()), "cmpc_set_observer");
   }
+  // The reference's controllers are values that NerveCenter copies into its
+  // tuple (nerve_center.h:95).  The constructor-argument form copies as a
+  // value; a stand-alone controller owns its device context (state estimate,
+  // u_old, warm start), which a copy would share, so it can only be moved.
+  DistributedController(const DistributedController& o) : constraints_(o.constraints_), M_(o.M_) {
+    if (o.dev_) throw Error("DistributedController: a stand-alone controller owns its device context; move it");
+  }
+  DistributedController& operator=(const DistributedController& o) {
+    if (o.dev_) throw Error("DistributedController: a stand-alone controller owns its device context; move it");
+    constraints_ = o.constraints_;
+    M_ = o.M_;
+    dev_.reset();
+    return *this;
+  }
+  DistributedController(DistributedController&&) noexcept = default;
+  DistributedController& operator=(DistributedController&&) noexcept = default;
+
   const InputConstraints& constraints() const { return constraints_; }
   const std::vector<double>& observer_matrix() const { return M_; }
 
@@ -264,7 +520,7 @@ class DistributedController {
     const std::vector<double> du0(D.L.nV, 0.0);
     const uint32_t ws0 = 0;
     Check(cmpc_set_state(D.ctx, u_init, du0.data(), &ws0), "cmpc_set_state");
-    Check(cmpc_observer_init_host(D.ctx, static_cast<int>(D.spec.plant), 1.0, 1.0, 0.05,
+    Check(cmpc_observer_init_host(D.ctx, static_cast<int>(D.spec.plant), D.spec.p_in, D.spec.p_out, D.spec.Ts,
                                   D.spec.input_order[D.s].data(), D.spec.out_idx[D.s].data(), x_init,
                                   full_u_old, y_init, dx_init),
           "cmpc_observer_init_host");
@@ -311,6 +567,32 @@ class DistributedController {
     Check(cmpc_get_observer_state(D.ctx, row.data()), "cmpc_get_observer_state");
     for (int i = 0; i < D.spec.ns; ++i) x_out[i] = row[i];
   }
+  /// The step's QP (H, f, G) as GenerateInitialQP built it.
+  QP GetQP() {
+    Device& D = dev();
+    QP qp;
+    qp.H.resize(static_cast<size_t>(D.L.nV) * D.L.nV);
+    qp.f.resize(D.L.nV);
+    qp.G.resize(static_cast<size_t>(D.L.nV) * D.L.nVo);
+    Check(cmpc_download_qp(D.ctx, qp.H.data(), qp.f.data(), D.L.nVo ? qp.G.data() : nullptr), "cmpc_download_qp");
+    return qp;
+  }
+  /// The lin record the last build read (the linearisation at the estimate,
+  /// the augmented state, y_prev; cmpc_layout) and this controller's u_old_
+  /// (nu_tot, its own input order).
+  std::vector<double> GetLinRecord() {
+    Device& D = dev();
+    std::vector<double> rec(D.L.rec_len);
+    Check(cmpc_download_lin(D.ctx, rec.data()), "cmpc_download_lin");
+    return rec;
+  }
+  std::vector<double> GetUOld() {
+    Device& D = dev();
+    std::vector<double> u(D.spec.nu_tot), du(D.L.nV);
+    uint32_t ws = 0;
+    Check(cmpc_get_state(D.ctx, u.data(), du.data(), &ws), "cmpc_get_state");
+    return u;
+  }
   /// status word and working-set change count of the last GetInput
   int last_status() { return dev().status; }
   int last_nwsr() { return dev().nwsr; }
@@ -334,7 +616,7 @@ class DistributedController {
   }
   InputConstraints constraints_;
   std::vector<double> M_;
-  std::shared_ptr<Device> dev_;
+  std::unique_ptr<Device> dev_;
 };
 
 // ControllerInterface<System> (include/controller_interface.h:18-50): the
@@ -482,7 +764,7 @@ class NerveCenter : public ControllerInterface {
       std::vector<double> dx;
       if (dx_init)
         for (int s = 0; s < spec_.S(); ++s) dx.insert(dx.end(), dx_init, dx_init + L_.ntot);
-      Check(cmpc_observer_init_host(ctx_, static_cast<int>(spec_.plant), 1.0, 1.0, 0.05, io.data(),
+      Check(cmpc_observer_init_host(ctx_, static_cast<int>(spec_.plant), spec_.p_in, spec_.p_out, spec_.Ts, io.data(),
                                     oi.data(), x_init, u_init_full, y_init,
                                     dx_init ? dx.data() : nullptr),
             "cmpc_observer_init_host");
@@ -605,7 +887,7 @@ class NerveCenter : public ControllerInterface {
   void FillRecords(const double* x, const double* u_full, const double* dx_aug, const double* y) {
     for (int s = 0; s < spec_.S(); ++s) {
       double* r = rec_.data() + static_cast<size_t>(s) * L_.rec_len;
-      Check(cmpc_plant_lin_record(static_cast<int>(spec_.plant), 1.0, 1.0, 0.05, x, u_full,
+      Check(cmpc_plant_lin_record(static_cast<int>(spec_.plant), spec_.p_in, spec_.p_out, spec_.Ts, x, u_full,
                                   spec_.input_order[s].data(), spec_.out_idx[s].data(), &d_, r),
             "cmpc_plant_lin_record");
       for (int i = 0; i < L_.naug; ++i) r[L_.off_x + i] = dx_aug ? dx_aug[i] : 0.0;

@@ -9,12 +9,18 @@
 //   UpdateUOld, SendUHelper: UpdateU(du with only the own inputs set),
 // and checks, step by step, that the applied inputs, the move plans, the QP
 // status words and every controller's GetStateEstimate equal NerveCenter's
+// bit for bit.  Beside each controller runs a DistributedSolver (the
+// reference's MpcQpSolver / DistributedSolver API, mpc_qp_solver.h:53-97,
+// distributed_solver.h:69-94) on the controller's own lin record and u_old:
+// its GenerateDistributedQP must equal the controller's QP, and every
+// UpdateAndSolveQP (SolveQP for a full controller) the controller's GetInput,
 // bit for bit.
 //
 // usage: distributed_controller_loop <setup-file> <par|ser> <cent|coop|ncoop> [p] [steps]
 // Prints one line per step; exit 0 if every step matched, 3 otherwise.
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -89,6 +95,26 @@ int main(int argc, char** argv) {
     nc.Initialize(x0.data(), u0.data(), u_off.data(), y0.data());
     for (int s = 0; s < S; ++s) ctrl[s].Initialize(x0.data(), u0.data(), u_off.data(), y0.data());
 
+    // (c) a DistributedSolver per sub-controller on the controller's records
+    std::vector<DistributedSolver> ds;
+    for (int s = 0; s < S; ++s) {
+      std::vector<double> uw(nu * nu), yr(static_cast<size_t>(p) * spec.ny);
+      for (int a = 0; a < nu; ++a)
+        for (int b = 0; b < nu; ++b) uw[a * nu + b] = setup.uwt[spec.input_order[s][a] * nut + spec.input_order[s][b]];
+      for (int i = 0; i < p; ++i)
+        for (int o = 0; o < spec.ny; ++o) yr[i * spec.ny + o] = y_ref[i * spec.n_outputs + spec.out_idx[s][o]];
+      ds.emplace_back(spec, s, ics[s], yr, uw, std::vector<double>(ywt[s], ywt[s] + blk));
+    }
+    bool solver_equal = true;
+    auto same_qp = [](const QP& a, const QP& b) { return a.H == b.H && a.f == b.f && a.G == b.G; };
+    std::vector<QP> qps(S);
+    for (int s = 0; s < S; ++s) {  // InitializeQPProblem on the initial QP
+      const std::vector<double> uo = ctrl[s].GetUOld();
+      ds[s].GenerateDistributedQP(&qps[s], ctrl[s].GetLinRecord().data(), uo.data());
+      solver_equal = solver_equal && same_qp(qps[s], ctrl[s].GetQP());
+      ds[s].InitializeQPProblem(qps[s], uo.data());
+    }
+
     // NerveCenter's own state for the hand-driven loop (nerve_center.h:71-75)
     std::vector<double> u_old(nut, 0.0), du_old(static_cast<size_t>(S) * nV, 0.0);
     bool all_equal = true;
@@ -100,7 +126,13 @@ int main(int argc, char** argv) {
       // (b) GetNextInputWithTiming's body with the per-object calls
       std::vector<double> u_full(u_off);
       for (int c = 0; c < nut; ++c) u_full[spec.plant_input_index[c]] += u_old[c];
-      for (int s = 0; s < S; ++s) ctrl[s].GenerateInitialQP(y.data(), u_full.data());
+      std::vector<std::vector<double>> uo_s(S);
+      for (int s = 0; s < S; ++s) {
+        ctrl[s].GenerateInitialQP(y.data(), u_full.data());
+        uo_s[s] = ctrl[s].GetUOld();
+        ds[s].GenerateDistributedQP(&qps[s], ctrl[s].GetLinRecord().data(), uo_s[s].data());
+        solver_equal = solver_equal && same_qp(qps[s], ctrl[s].GetQP());
+      }
       std::vector<double> du_prev(du_old), du_new(du_old.size());
       std::vector<int> status(S, 0);
       for (int i = 0; i < K; ++i) {
@@ -110,6 +142,14 @@ int main(int argc, char** argv) {
             if (s2 != s) du_last.insert(du_last.end(), du_prev.begin() + s2 * nV, du_prev.begin() + (s2 + 1) * nV);
           ctrl[s].GetInput(du_new.data() + s * nV, du_last.empty() ? nullptr : du_last.data());
           status[s] = ctrl[s].last_status();
+          // the same solve through the reference's solver API, on a copy of
+          // the step's QP (distributed_controller.h:214)
+          QP copy = qps[s];
+          std::vector<double> du_ds;
+          if (du_last.empty()) du_ds = ds[s].SolveQP(copy, uo_s[s].data());
+          else ds[s].UpdateAndSolveQP(&copy, &du_ds, uo_s[s].data(), du_last.data());
+          solver_equal = solver_equal && ds[s].last_status() == status[s] &&
+                         std::equal(du_ds.begin(), du_ds.end(), du_new.begin() + s * nV);
         }
         du_prev = du_new;
       }
@@ -139,8 +179,9 @@ int main(int argc, char** argv) {
       for (double v : u_old) std::printf(" %.9g", v);
       std::printf("  status");
       for (int v : status) std::printf(" %d", v);
-      std::printf("  %s (max |du| %.3g)\n", eq ? "equal" : "DIFFERENT", dmax);
-      all_equal = all_equal && eq;
+      std::printf("  %s (max |du| %.3g)  solver API %s\n", eq ? "equal" : "DIFFERENT", dmax,
+                  solver_equal ? "equal" : "DIFFERENT");
+      all_equal = all_equal && eq && solver_equal;
     }
     return all_equal ? 0 : 3;
   } catch (const std::exception& e) {

@@ -18,6 +18,9 @@ import _oracle as O
 from cmpc.coupled import coupled_jacobi, coupling_weights, others, synthetic_g_ext
 
 S_TOTAL, B, K = 8, 6, 9
+# SURVEY config 4's real partition (8 ranks x 8 sub-controllers), rehearsed on
+# CPU with a small batch
+S_TOTAL8, B8 = 64, 2
 
 
 def test_coupling_weights_are_layout_independent():
@@ -45,14 +48,14 @@ def test_rank_major_plan_indexing():
 
 # ---- the loop with the oracle's solver as the compute ----------------------
 
-def problem():
+def problem(S_total=S_TOTAL, Bn=B):
     import cmpc
     from cmpc.configs import reference_setup
     from cmpc.synthetic import synthetic_batch
     from cmpc._abi import CmpcDims
     cfg = cmpc.reference_config("par", "coop", p=20)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
-    nrec = B * S_TOTAL                     # record (b, s_global) = b * S_TOTAL + s
+    nrec = Bn * S_total                    # record (b, s_global) = b * S_total + s
     lin, u_old, _, _ = synthetic_batch(cfg, nrec // cfg.S, seed=12)
     dims = CmpcDims.from_config(cfg, 1)
     H, f, G = [], [], []
@@ -63,23 +66,23 @@ def problem():
     return cfg, arr, np.array(H), np.array(f), np.array(G), u_old
 
 
-def oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather):
+def oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather, S_total=S_TOTAL, Bn=B):
     """This rank's QPs through coupled_jacobi with or_qp_solve (the oracle)."""
-    sl = S_TOTAL // world
-    glob = [b * S_TOTAL + rank * sl + i for b in range(B) for i in range(sl)]
-    Gx = synthetic_g_ext(G[glob], S_TOTAL, sl, rank * sl).reshape(4, -1, len(glob))
+    sl = S_total // world
+    glob = [b * S_total + rank * sl + i for b in range(Bn) for i in range(sl)]
+    Gx = synthetic_g_ext(G[glob], S_total, sl, rank * sl).reshape(4, -1, len(glob))
     ws = np.zeros(len(glob), np.uint32)
     nu = cfg.nu
 
     def solve(du_all, apply):
-        du_all = du_all.reshape(world, B, sl, 4)
+        du_all = du_all.reshape(world, Bn, sl, 4)
         out = np.zeros((len(glob), 4))
         for i, q in enumerate(glob):
             b, li = divmod(i, sl)
             s_cfg = q % cfg.S
-            d = others(du_all, b, rank * sl + li, S_TOTAL, sl)
+            d = others(du_all, b, rank * sl + li, S_total, sl)
             fk = [float(v) for v in f[q]]
-            for j in range(S_TOTAL - 1):          # the kernel's order: j, then a, then v
+            for j in range(S_total - 1):          # the kernel's order: j, then a, then v
                 for a in range(4):
                     for v in range(4):
                         fk[a] = fk[a] + float(Gx[a, j * 4 + v, i]) * float(d[j * 4 + v])
@@ -100,21 +103,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _cpu_worker(rank, world, port, q):
+def _cpu_worker(rank, world, port, q, S_total=S_TOTAL, Bn=B):
     import torch
     import torch.distributed as dist
+    torch.set_num_threads(1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg, arr, H, f, G, u_old = problem()
+        cfg, arr, H, f, G, u_old = problem(S_total, Bn)
 
         def gather(du_local):
             parts = [torch.zeros(du_local.shape, dtype=torch.float64) for _ in range(world)]
             dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(du_local)))
             return torch.stack(parts).numpy()
 
-        du = oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather)
+        du = oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather, S_total, Bn)
         allp = gather(du)
         if rank == 0:
             q.put(allp)
@@ -122,24 +126,66 @@ def _cpu_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_loop_two_ranks_gloo_equals_one():
-    world = 2
+def _sharded_equals_one(world, S_total, Bn):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_cpu_worker, args=(r, world, port, q, S_total, Bn)) for r in range(world)]
     for p in ps:
         p.start()
-    got = q.get(timeout=600)
+    try:
+        got = q.get(timeout=600)
+    finally:
+        for p in ps:
+            p.join(timeout=120)
     for p in ps:
-        p.join(timeout=60)
         assert p.exitcode == 0
-    cfg, arr, H, f, G, u_old = problem()
-    ref = oracle_loop(cfg, arr, H, f, G, u_old, 0, 1, lambda d: d[None])
-    # rank-major [world][B][sl][4] -> global [B][S_TOTAL][4]
-    sl = S_TOTAL // world
-    got = got.reshape(world, B, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
+    cfg, arr, H, f, G, u_old = problem(S_total, Bn)
+    ref = oracle_loop(cfg, arr, H, f, G, u_old, 0, 1, lambda d: d[None], S_total, Bn)
+    # rank-major [world][B][sl][4] -> global [B][S_total][4]
+    sl = S_total // world
+    got = got.reshape(world, Bn, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
     assert np.array_equal(got, ref)
+    return ref
+
+
+def test_sharded_loop_two_ranks_gloo_equals_one():
+    _sharded_equals_one(2, S_TOTAL, B)
+
+
+def test_sharded_loop_config4_partition_eight_ranks_gloo_equals_one():
+    """SURVEY config 4's own partition: 8 ranks x S_local = 8 sub-controllers,
+    S_total = 64 per scenario (rank-major plan indexing over 8 ranks), the
+    plans all-gathered over gloo once per Jacobi iteration, the oracle's
+    solver as the compute: bit-exact with one process running all 64."""
+    ref = _sharded_equals_one(8, S_TOTAL8, B8)
+    assert np.abs(ref).max() > 0  # the coupling moved the plans
+
+
+def test_abi_refuses_coupled_reads_beyond_the_callers_buffers():
+    """cmpc_coupled_iterate's own checks (cmpc_coupled_validate, host only):
+    a one-rank plan buffer for S_total = 64 sub-controllers with S_local = 8
+    (the layout that faulted the GPU in round 3) is refused in C with an
+    error naming du_all, as is a G_ext shorter than the kernel reads."""
+    import ctypes
+    import cmpc
+    from cmpc._abi import CmpcDims, load_library
+    lib = load_library()
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    S_local, Bsc = 8, 4096
+    nqp = Bsc * S_local
+    dims = CmpcDims.from_config(cfg, nqp // cfg.S)
+    nV = cfg.nV
+    g_len = nV * 63 * nV * nqp
+    one_rank = nqp * nV
+    rc = lib.cmpc_coupled_validate(ctypes.byref(dims), 64, S_local, 0, g_len, one_rank)
+    assert rc == -1
+    assert b"du_all" in lib.cmpc_last_error()
+    rc = lib.cmpc_coupled_validate(ctypes.byref(dims), 64, S_local, 0, g_len - 1, 64 * Bsc * nV)
+    assert rc == -1 and b"G_ext" in lib.cmpc_last_error()
+    assert lib.cmpc_coupled_validate(ctypes.byref(dims), 64, S_local, 0, g_len, 64 * Bsc * nV) == 0
+    assert lib.cmpc_coupled_validate(ctypes.byref(dims), 8, S_local, 0, nV * 7 * nV * nqp, one_rank) == 0
+    assert lib.cmpc_coupled_validate(ctypes.byref(dims), 64, S_local, 64, g_len, 64 * Bsc * nV) == -1
 
 
 # ---- GPU: the product kernel -----------------------------------------------
