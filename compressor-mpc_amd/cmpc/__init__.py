@@ -16,7 +16,9 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE,
+from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_SOLVE_AUTO, CMPC_SOLVE_LANE,
+                   CMPC_SOLVE_ROWS, CMPC_STEP_AUTO, CMPC_STEP_FUSED, CMPC_STEP_SPLIT, CMPC_KERNEL_STEP,
+                   CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE,
                    CMPC_KERNEL_PRODUCE, CMPC_KERNEL_OBSERVE_POST, CMPC_KERNEL_OBSERVE_PRIOR, CMPC_QP_INFEASIBLE,
                    CMPC_QP_MAX_NWSR, CMPC_QP_NOT_PD, CMPC_QP_NONFINITE, CMPC_QP_OK, CMPC_TRACE, CmpcDims,
                    CmpcLayout, bptr, check, dptr, iptr, load_library, uptr)
@@ -268,6 +270,27 @@ class Context:
         check(min(v, 0), "cmpc_last_build_kernel")
         return v
 
+
+    def set_solve_variant(self, variant: int):
+        """CMPC_SOLVE_AUTO / CMPC_SOLVE_LANE (one QP per lane) / CMPC_SOLVE_ROWS
+        (one QP per 16-lane row): the kernel of iterate / init_warmstart."""
+        check(self.lib.cmpc_set_solve_variant(self._h, int(variant)), "cmpc_set_solve_variant")
+
+    def last_solve_kernel(self) -> int:
+        """CMPC_SOLVE_LANE / CMPC_SOLVE_ROWS: the kernel the last solve ran."""
+        v = self.lib.cmpc_last_solve_kernel(self._h)
+        check(min(v, 0), "cmpc_last_solve_kernel")
+        return v
+
+    def set_step_variant(self, variant: int):
+        """CMPC_STEP_AUTO / CMPC_STEP_SPLIT (build + iterate launches) /
+        CMPC_STEP_FUSED (one launch: the build kernel runs the iterations)."""
+        check(self.lib.cmpc_set_step_variant(self._h, int(variant)), "cmpc_set_step_variant")
+
+    def last_step_fused(self) -> bool:
+        v = self.lib.cmpc_last_step_fused(self._h)
+        check(min(v, 0), "cmpc_last_step_fused")
+        return bool(v)
     def init_warmstart(self):
         check(self.lib.cmpc_init_warmstart(self._h), "cmpc_init_warmstart")
 

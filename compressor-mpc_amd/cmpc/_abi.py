@@ -31,11 +31,18 @@ CMPC_KERNEL_ITERATE = 1
 CMPC_KERNEL_PRODUCE = 2
 CMPC_KERNEL_OBSERVE_POST = 3
 CMPC_KERNEL_OBSERVE_PRIOR = 4
-CMPC_KERNEL_COUNT = 5
+CMPC_KERNEL_STEP = 5
+CMPC_KERNEL_COUNT = 6
 
 CMPC_BUILD_AUTO = 0
 CMPC_BUILD_WAVE = 1
 CMPC_BUILD_ROWS = 2
+CMPC_SOLVE_AUTO = 0
+CMPC_SOLVE_LANE = 1
+CMPC_SOLVE_ROWS = 2
+CMPC_STEP_AUTO = 0
+CMPC_STEP_SPLIT = 1
+CMPC_STEP_FUSED = 2
 
 
 class CmpcDims(ctypes.Structure):
@@ -86,7 +93,7 @@ EXPORTS = (
     "cmpc_layout_of", "cmpc_create", "cmpc_destroy", "cmpc_set_stream",
     "cmpc_last_error", "cmpc_get_layout", "cmpc_set_weights", "cmpc_set_constraints",
     "cmpc_set_reference", "cmpc_set_state", "cmpc_get_state", "cmpc_upload_lin",
-    "cmpc_lin_device", "cmpc_build", "cmpc_set_build_variant", "cmpc_rows_lds_model", "cmpc_last_build_kernel", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
+    "cmpc_lin_device", "cmpc_build", "cmpc_set_build_variant", "cmpc_rows_lds_model", "cmpc_last_build_kernel", "cmpc_set_solve_variant", "cmpc_last_solve_kernel", "cmpc_set_step_variant", "cmpc_last_step_fused", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
@@ -149,6 +156,10 @@ def load_library(path: str = LIB_PATH):
         "cmpc_build": ([c_void], ctypes.c_int),
         "cmpc_set_build_variant": ([c_void, ctypes.c_int], ctypes.c_int),
         "cmpc_last_build_kernel": ([c_void], ctypes.c_int),
+        "cmpc_set_solve_variant": ([c_void, ctypes.c_int], ctypes.c_int),
+        "cmpc_last_solve_kernel": ([c_void], ctypes.c_int),
+        "cmpc_set_step_variant": ([c_void, ctypes.c_int], ctypes.c_int),
+        "cmpc_last_step_fused": ([c_void], ctypes.c_int),
         "cmpc_rows_lds_model": ([P(CmpcDims), P(dbl), P(dbl), P(ctypes.c_int32)], ctypes.c_int),
         "cmpc_init_warmstart": ([c_void], ctypes.c_int),
         "cmpc_iterate": ([c_void, ctypes.c_int, u32], ctypes.c_int),

@@ -47,6 +47,7 @@
 
 #include "cmpc_internal.h"
 #include "rows_blocks.inc"
+#include "solve_rows.h"
 
 // Timing-only ablation switches (tools/ablate_rows.sh); the product build
 // uses CMPC_RX = 0.  1: no LDS hand-off in the loop, 3: no gather
@@ -106,7 +107,12 @@
 // WPE: waves per SIMD the register allocation targets (CMPC_ROWS_WPE = 3, 168
 // registers; 2 for layouts whose LDS admits no more than two waves per SIMD
 // anyway: 256 registers, no spills for ny = 4 / nV = 8 at long horizons)
-template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG, bool RING, int WPE = CMPC_ROWS_WPE>
+// FUSE (cmpc_step on small batches): after its QPs are built, the wave runs
+// their K Jacobi iterations itself (solve_rows.h), H, f and G handed from the
+// gather lanes to the solver's rows by lane shuffles; 1 plain, 2 with the
+// working-set trace.  The QPs are still stored (cmpc_download_qp).
+template <int NS, int NY, int NUT, int NU, int M, int ND, int WPG, bool RING, int WPE = CMPC_ROWS_WPE,
+          int FUSE = 0>
 __global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void cmpc_build_rows_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -586,6 +592,46 @@ void cmpc_build_rows_kernel(BuildParams P) {
         for (int a = 0; a < NV; ++a) out[NV * NV + NV + a * nVo + k2 * nuo + (c2 - NU)] = acc[a];  // G
       }
     }
+    if constexpr (FUSE > 0) {
+      // the row solver's layout: lane l < NV holds row l of H and of G and
+      // f[l].  Gather lane b = (k, c) holds column (k, c) of H, G or f (its
+      // acc[a] = entry a); H is exactly symmetric (acc_b[a] == acc_a[b]), so
+      // row l of H is the column the gather lane of column l holds, and
+      // H[l][c] = that lane's acc[c] + the R block entry, as stored above
+      constexpr int N = NV, NVO = M * (NUT - NU), NVOA = NVO > 0 ? NVO : 1, nuo = NUT - NU;
+      const int rb = lane & ~15;
+      const int lcol = (j < N) ? (j / NU) * NUT + (j % NU) : 0;
+      const double* uwt = uw_all + s * NU * NU;
+      double Hl[N], Fv[N], Gl[NVOA];
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        const double a = __shfl(acc[c], rb + lcol, 64);
+        const double rw = (j < N && c / NU == j / NU) ? uwt[(j % NU) * NU + (c % NU)] : 0.0;
+        Hl[c] = (j < N) ? a + rw : 0.0;
+      }
+      static_for<N>([&](auto A) {
+        constexpr int a = decltype(A)::value;
+        Fv[a] = rbc<NG - 1>(acc[a]);  // f from the z lane
+      });
+#pragma unroll
+      for (int c = 0; c < NVOA; ++c) Gl[c] = 0.0;
+      if constexpr (NVO > 0) {
+        static_for<NVO>([&](auto C) {
+          constexpr int c = decltype(C)::value;
+          constexpr int lg = (c / nuo) * NUT + NU + (c % nuo);  // gather lane of G's column c
+          double col[N];
+          static_for<N>([&](auto A) {
+            constexpr int a = decltype(A)::value;
+            col[a] = rbc<lg>(acc[a]);
+          });
+          Gl[c] = (j < N) ? sel<N>(col, j) : 0.0;
+        });
+      }
+      const double f_l = (j < N) ? sel<N>(Fv, j) : 0.0;
+      // the wave's region is dead until the next group's staging: H^-1 scratch
+      rows_solve_qp<N, NU, NVO, FUSE == 2, false>(P.sv, qq, qv, s, j, rb - 16 * s, Hl, f_l, Gl,
+                                                  wreg + R * N * N);
+    }
     __builtin_amdgcn_wave_barrier();
     CMPC_T(4)  // epilogue
 #if CMPC_ROWS_TIMING
@@ -616,9 +662,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
 // ---------------------------------------------------------------------------
 // Waves per workgroup (4, or 2 where that holds 1.5x the resident waves;
 // cmpc_rows_waves_per_group in rows_layout.cpp).
-template <int NS, int NY, int NU, int M, int WPG, bool RING, int WPE = CMPC_ROWS_WPE>
+template <int NS, int NY, int NU, int M, int WPG, bool RING, int WPE = CMPC_ROWS_WPE, int FUSE = 0>
 static int rows_launch(const BuildParams& P, hipStream_t s) {
-  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG, RING, WPE>;
+  auto kern = cmpc_build_rows_kernel<NS, NY, 4, NU, M, 2, WPG, RING, WPE, FUSE>;
   const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * WPG);
   if (lds > 160 * 1024) return -1;
   if (lds > 64 * 1024)
@@ -655,6 +701,36 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
     }                                                                                  \
     return -1;                                                                         \
   }
+
+// fused build + K iterations (small batches): four-wave workgroups at two
+// waves per SIMD (256 registers: the solver's state on top of the build's)
+#define ROWS_FUSED_CASE(NS_, NY_, NU_, M_)                                            \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
+    if (cmpc_rows_waves_per_group(P.rows) != 4) return -1;                           \
+    if (P.rows.per_wave < 4 * (NU_ * M_) * (NU_ * M_)) return -1;                    \
+    if (ring) {                                                                        \
+      if (trace) return rows_launch<NS_, NY_, NU_, M_, 4, true, 2, 2>(P, s);          \
+      return rows_launch<NS_, NY_, NU_, M_, 4, true, 2, 1>(P, s);                     \
+    }                                                                                  \
+    if (trace) return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 2>(P, s);           \
+    return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 1>(P, s);                      \
+  }
+
+int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!P.rows.ok || P.S < 1 || 4 % P.S) return -1;
+  bool ring = false;
+  for (int c = 0; c < CMPC_MAX_INPUTS; ++c) ring = ring || P.rows.ring[c] > 0;
+  if (!ring && P.rows.nseg > 2 * 2) return -1;
+  const bool trace = P.sv.trace != nullptr;
+  ROWS_FUSED_CASE(11, 3, 2, 2)  // parallel coop
+  ROWS_FUSED_CASE(11, 2, 2, 2)  // parallel ncoop
+  ROWS_FUSED_CASE(11, 3, 4, 2)  // parallel centralized
+  ROWS_FUSED_CASE(10, 2, 2, 2)  // serial ncoop
+  ROWS_FUSED_CASE(10, 4, 2, 2)  // serial coop
+  ROWS_FUSED_CASE(10, 4, 4, 2)  // serial centralized
+  return -1;
+}
 
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
   hipStream_t s = (hipStream_t)stream;

@@ -177,6 +177,10 @@ struct cmpc_ctx {
   // build kernel selection (cmpc_set_build_variant)
   int build_variant = CMPC_BUILD_AUTO;
   int last_build = 0;  // kernel launched by the last cmpc_build
+  int solve_variant = CMPC_SOLVE_AUTO;  // cmpc_set_solve_variant
+  int last_solve = 0;                   // kernel launched by the last solve
+  int step_variant = CMPC_STEP_AUTO;    // cmpc_set_step_variant
+  int last_step_fused = 0;
   // timing
   int timing = 0;  // bit k: kernel k (CMPC_KERNEL_*) is timed
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[CMPC_KERNEL_COUNT];
@@ -1378,13 +1382,42 @@ int cmpc_last_build_kernel(cmpc_ctx* c) {
   return c->last_build;
 }
 
+static int build_params(cmpc_ctx* c, BuildParams& P);
+
 int cmpc_build(cmpc_ctx* c) {
   if (!c) return fail("null context");
   if (ensure_cfg(c)) return -1;
   HIP_TRY(hipSetDevice(c->device));
   const cmpc_dims& d = c->d;
-  const cmpc_layout& L = c->L;
   BuildParams P;
+  if (build_params(c, P)) return -1;
+  TimedLaunch tl(c, CMPC_KERNEL_BUILD);
+  if (tl.begin()) return -1;
+  int rc = -1;
+  // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
+  // than the one-QP-per-wave kernel for every plant/controller type at
+  // p = 20, 50, 100, 200: tools/gpu_build_table.sh, DESIGN.md §3.0) and the
+  // batch gives it at least one wave per SIMD; else
+  // the one-QP-per-wave kernel, which has four times the waves for a small
+  // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
+  const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
+  if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_fill))
+    rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
+  if (rc && c->build_variant == CMPC_BUILD_ROWS)
+    return fail("row-layout build kernel not available for these dimensions");
+  c->last_build = CMPC_BUILD_ROWS;
+  if (rc) {
+    if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
+      return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
+    c->last_build = CMPC_BUILD_WAVE;
+  }
+  if (check_launch("build kernel")) return -1;
+  return tl.end();
+}
+
+static int build_params(cmpc_ctx* c, BuildParams& P) {
+  const cmpc_dims& d = c->d;
+  const cmpc_layout& L = c->L;
   std::memset(&P, 0, sizeof P);
   P.lin = c->lin_bound ? c->lin_bound : c->lin;
   P.cfg = c->cfg;
@@ -1431,28 +1464,53 @@ int cmpc_build(cmpc_ctx* c) {
     P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
   }
   cmpc_rows_layout(d, L.nd, L.nobs, L.rec_len, &P.rows);  // cached per dimension set
-  TimedLaunch tl(c, CMPC_KERNEL_BUILD);
-  if (tl.begin()) return -1;
-  int rc = -1;
-  // AUTO: the row kernel wherever its LDS fits (measured as fast or faster
-  // than the one-QP-per-wave kernel for every plant/controller type at
-  // p = 20, 50, 100, 200: tools/gpu_build_table.sh, DESIGN.md §3.0) and the
-  // batch gives it at least one wave per SIMD; else
-  // the one-QP-per-wave kernel, which has four times the waves for a small
-  // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
-  const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
-  if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_fill))
-    rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
-  if (rc && c->build_variant == CMPC_BUILD_ROWS)
-    return fail("row-layout build kernel not available for these dimensions");
-  c->last_build = CMPC_BUILD_ROWS;
-  if (rc) {
-    if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
-      return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
-    c->last_build = CMPC_BUILD_WAVE;
+  return 0;
+}
+
+// working-set trace buffers for K iterations of every QP (CMPC_TRACE)
+static int trace_buffers(cmpc_ctx* c, int K) {
+  const size_t need = (size_t)c->nqp * K * 16;
+  if (need > c->trace_cap) {
+    if (c->trace) HIP_TRY(hipFree(c->trace));
+    if (c->ntrace) HIP_TRY(hipFree(c->ntrace));
+    c->trace = nullptr;
+    c->ntrace = nullptr;
+    HIP_TRY(hipMalloc(&c->trace, need));
+    HIP_TRY(hipMalloc(&c->ntrace, sizeof(int32_t) * (size_t)c->nqp * K));
+    c->trace_cap = need;
   }
-  if (check_launch("build kernel")) return -1;
-  return tl.end();
+  c->trace_K = K;
+  return 0;
+}
+
+int cmpc_set_solve_variant(cmpc_ctx* c, int variant) {
+  if (!c) return fail("null context");
+  if (variant != CMPC_SOLVE_AUTO && variant != CMPC_SOLVE_LANE && variant != CMPC_SOLVE_ROWS)
+    return fail("cmpc_set_solve_variant: unknown variant");
+  c->solve_variant = variant;
+  return 0;
+}
+
+int cmpc_last_solve_kernel(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  return c->last_solve;
+}
+
+// the iterate / init / get-input launch through the selected solve kernel
+static int launch_solve(cmpc_ctx* c, const SolveParams& P, const char* who) {
+  const int nV = c->L.nV, nu = c->d.nu, nVo = c->L.nVo;
+  const bool want_rows = c->solve_variant == CMPC_SOLVE_ROWS ||
+                         (c->solve_variant == CMPC_SOLVE_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP);
+  if (want_rows && cmpc_launch_solve_rows(P, nV, nu, nVo, c->stream) == 0) {
+    c->last_solve = CMPC_SOLVE_ROWS;
+    return 0;
+  }
+  if (c->solve_variant == CMPC_SOLVE_ROWS)
+    return fail(std::string(who) + ": row solve kernel not available for these dimensions (S must divide 4)");
+  if (cmpc_launch_solve(P, nV, nu, nVo, c->stream))
+    return fail(std::string(who) + ": solve kernel not instantiated for these dimensions");
+  c->last_solve = CMPC_SOLVE_LANE;
+  return 0;
 }
 
 int cmpc_init_warmstart(cmpc_ctx* c) {
@@ -1463,8 +1521,7 @@ int cmpc_init_warmstart(cmpc_ctx* c) {
   solve_params(c, &P);
   P.init = 1;
   cmpc_launch_events = LaunchEvents{};  // untimed (a failed timed launch may have left them set)
-  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
-    return fail("solve kernel not instantiated for these dimensions");
+  if (launch_solve(c, P, "cmpc_init_warmstart")) return -1;
   return check_launch("init kernel");
 }
 
@@ -1481,24 +1538,13 @@ int cmpc_iterate(cmpc_ctx* c, int K, uint32_t flags) {
   P.K = K;
   P.flags = flags;
   if ((flags & CMPC_TRACE) && K > 0) {
-    const size_t need = (size_t)c->nqp * K * 16;
-    if (need > c->trace_cap) {
-      if (c->trace) HIP_TRY(hipFree(c->trace));
-      if (c->ntrace) HIP_TRY(hipFree(c->ntrace));
-      c->trace = nullptr;
-      c->ntrace = nullptr;
-      HIP_TRY(hipMalloc(&c->trace, need));
-      HIP_TRY(hipMalloc(&c->ntrace, sizeof(int32_t) * (size_t)c->nqp * K));
-      c->trace_cap = need;
-    }
+    if (trace_buffers(c, K)) return -1;
     P.trace = c->trace;
     P.ntrace = c->ntrace;
-    c->trace_K = K;
   }
   TimedLaunch tl(c, CMPC_KERNEL_ITERATE);
   if (tl.begin()) return -1;
-  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
-    return fail("solve kernel not instantiated for these dimensions");
+  if (launch_solve(c, P, "cmpc_iterate")) return -1;
   if (check_launch("iterate kernel")) return -1;
   return tl.end();
 }
@@ -1519,8 +1565,7 @@ int cmpc_get_input(cmpc_ctx* c, const double* du_last, uint32_t flags) {
   P.du_other = du_last;
   TimedLaunch tl(c, CMPC_KERNEL_ITERATE);
   if (tl.begin()) return -1;
-  if (cmpc_launch_solve(P, c->L.nV, c->d.nu, c->L.nVo, c->stream))
-    return fail("cmpc_get_input: solve kernel not instantiated for these dimensions");
+  if (launch_solve(c, P, "cmpc_get_input")) return -1;
   if (check_launch("get-input kernel")) return -1;
   return tl.end();
 }
@@ -1631,7 +1676,68 @@ int cmpc_coupled_iterate(cmpc_ctx* c, int S_total, int S_local, int s_offset, co
   return tl.end();
 }
 
+int cmpc_set_step_variant(cmpc_ctx* c, int variant) {
+  if (!c) return fail("null context");
+  if (variant != CMPC_STEP_AUTO && variant != CMPC_STEP_SPLIT && variant != CMPC_STEP_FUSED)
+    return fail("cmpc_set_step_variant: unknown variant");
+  c->step_variant = variant;
+  return 0;
+}
+
+int cmpc_last_step_fused(cmpc_ctx* c) {
+  if (!c) return fail("null context");
+  return c->last_step_fused;
+}
+
+// GetNextInputWithTiming's device part: the build, then K Jacobi iterations.
+// On small batches one fused launch (the build kernel solves its own QPs:
+// no launch gap, no HBM round trip of H, f, G); else cmpc_build + cmpc_iterate.
 int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
+  if (!c) return fail("null context");
+  if (K < 0) return fail("K must be >= 0");
+  const bool want = c->step_variant == CMPC_STEP_FUSED ||
+                    (c->step_variant == CMPC_STEP_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP &&
+                     c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);
+  if (want && K > 0 && c->L.nuo == (c->d.S - 1) * c->d.nu) {
+    if (ensure_cfg(c)) return -1;
+    HIP_TRY(hipSetDevice(c->device));
+    BuildParams P;
+    if (build_params(c, P)) return -1;
+    solve_params(c, &P.sv);
+    P.sv.K = K;
+    P.sv.flags = flags;
+    if ((flags & CMPC_TRACE) && trace_buffers(c, K)) return -1;
+    if (flags & CMPC_TRACE) {
+      P.sv.trace = c->trace;
+      P.sv.ntrace = c->ntrace;
+    }
+    TimedLaunch tl(c, CMPC_KERNEL_STEP);
+    if (tl.begin()) return -1;
+    const cmpc_dims& d = c->d;
+    // the build kernel AUTO would pick: one QP per wave below one row group per
+    // SIMD (centralized only, S = 1), else four QPs per wave
+    const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
+    int rc = -1, kind = CMPC_BUILD_ROWS;
+    if (d.S == 1 && !rows_fill) {
+      rc = cmpc_launch_step_wave(P, d.ns, d.ny, d.nu, d.m, c->stream);
+      kind = CMPC_BUILD_WAVE;
+    }
+    if (rc) {
+      rc = cmpc_launch_step_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
+      kind = CMPC_BUILD_ROWS;
+    }
+    if (rc == 0) {
+      if (check_launch("fused step kernel")) return -1;
+      c->last_build = kind;
+      c->last_solve = CMPC_SOLVE_ROWS;
+      c->last_step_fused = 1;
+      return tl.end();
+    }
+    cmpc_launch_events = LaunchEvents{};
+    if (c->step_variant == CMPC_STEP_FUSED)
+      return fail("cmpc_step: no fused step kernel for these dimensions");
+  }
+  c->last_step_fused = 0;
   if (cmpc_build(c)) return -1;
   return cmpc_iterate(c, K, flags);
 }

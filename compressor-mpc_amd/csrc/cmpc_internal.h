@@ -31,6 +31,9 @@ inline void cmpc_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t
 #define CMPC_ROWS_NSEG 16        // loop segment bounds of the row build kernel
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 #define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
+#ifndef CMPC_SOLVE_ROWS_MAX_QP
+#define CMPC_SOLVE_ROWS_MAX_QP 16384  // CMPC_SOLVE_AUTO: the row solve kernel below this many QPs
+#endif
 
 // Per sub-controller configuration block in device memory (doubles):
 //   [lwt  : ny*ny ]  L_W' with ywt = L_W L_W' (upper triangular)
@@ -63,6 +66,25 @@ struct RowsLayout {
   int nseg, seg[CMPC_ROWS_NSEG];  // ascending distinct D, p - D and wrap steps inside (0, p)
 };
 
+struct SolveParams {
+  const double* qp;
+  const double* cfg;
+  double* u_old;      // nqp * nu_tot
+  double* du_old;     // nqp * nV
+  uint32_t* ws;       // nqp
+  double* du;         // nqp * nV
+  int32_t* status;    // nqp
+  int32_t* nwsr;      // nqp
+  uint8_t* trace;     // nqp * K * 16 or null
+  int32_t* ntrace;    // nqp * K or null
+  int nqp, S, K, nu_tot, qp_len;
+  CfgOffsets co;
+  uint32_t flags;
+  int init;           // 1: InitializeQPProblem (cold, f only, ws only)
+  const double* du_other;  // nqp * nVo other controllers' plans (cmpc_get_input), or null:
+                           // the in-scenario exchange of cmpc_iterate
+};
+
 struct BuildParams {
   const double* lin;     // nqp * rec_len
   const double* cfg;     // S * cfg.len
@@ -92,26 +114,12 @@ struct BuildParams {
   int grid;                      // workgroups needed (one QP per wave); launcher caps it
   int cus;                       // compute units of the device
   RowsLayout rows;               // row-layout kernel (four QPs per wave)
+  // fused step (cmpc_step on small batches): the K Jacobi iterations run in
+  // the build kernel on the QPs it just built (solve_rows.h), with these
+  // parameters (sv.qp unused: H, f, G stay in registers)
+  SolveParams sv;
 };
 
-struct SolveParams {
-  const double* qp;
-  const double* cfg;
-  double* u_old;      // nqp * nu_tot
-  double* du_old;     // nqp * nV
-  uint32_t* ws;       // nqp
-  double* du;         // nqp * nV
-  int32_t* status;    // nqp
-  int32_t* nwsr;      // nqp
-  uint8_t* trace;     // nqp * K * 16 or null
-  int32_t* ntrace;    // nqp * K or null
-  int nqp, S, K, nu_tot, qp_len;
-  CfgOffsets co;
-  uint32_t flags;
-  int init;           // 1: InitializeQPProblem (cold, f only, ws only)
-  const double* du_other;  // nqp * nVo other controllers' plans (cmpc_get_input), or null:
-                           // the in-scenario exchange of cmpc_iterate
-};
 
 // Standalone batched solver (parity / KKT tests).
 struct QpBatchParams {
@@ -202,6 +210,11 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
 // Row-layout build kernel (build_rows.hip); -1 when not instantiated / not usable.
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
                            void* stream);
+// Fused step (build_rows.hip): the row build kernel running the K Jacobi
+// iterations of its QPs itself (P.sv); -1 when not available.
+int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream);
+// the same on the one-QP-per-wave build kernel (cmpc_kernels.hip; S = 1)
+int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream);
 // Waves per workgroup the row kernel launches with for layout R (4, 2 or 1;
 // 0: does not fit) (build_rows.hip).
 int cmpc_rows_waves_per_group(const RowsLayout& R);
@@ -214,6 +227,9 @@ void cmpc_rows_layout(const cmpc_dims& d, int nd, int nobs, int rec_len, RowsLay
 double cmpc_rows_layout_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave);
 int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
                       void* stream);
+// Row-layout iterate kernel (solve_rows.hip): one QP per 16-lane row;
+// -1 when not instantiated for these dimensions or S does not divide 4.
+int cmpc_launch_solve_rows(const SolveParams& P, int nV, int nu, int nVo, void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
 // Plant simulation (sim.hip)
 struct SimParams {

@@ -31,6 +31,7 @@
 
 #include "cmpc_internal.h"
 #include "dpp_blocks.inc"
+#include "solve_rows.h"
 
 // Ablation switches for timing experiments (tools/ablate.sh); the product
 // build uses CMPC_EXP = 0.
@@ -105,8 +106,13 @@
 // ---------------------------------------------------------------------------
 // build kernel
 // ---------------------------------------------------------------------------
-template <int NS, int NY, int NUT, int NU, int M, int ND>
-__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(4, 4)))
+// FUSE (cmpc_step on small centralized batches, S = 1): after a QP is built
+// its wave runs the K Jacobi iterations on it (solve_rows.h: row 0 is the
+// QP's solver row, rows 1-3 shadow it without stores); 1 plain, 2 with the
+// working-set trace.  The QP is still stored (cmpc_download_qp).
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE = 0>
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES)
+__attribute__((amdgpu_waves_per_eu(FUSE ? 1 : 4, FUSE ? 1 : 4)))
 void cmpc_build_kernel(BuildParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -460,6 +466,67 @@ void cmpc_build_kernel(BuildParams P) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) red_w[k] = acc[k];
     }
+    if constexpr (FUSE > 0) {
+      // every row forms the totals (row 0's partial through LDS as well), in
+      // the order row 0 uses below: the solver's four rows see the same H
+      if (row == 0 && col < NG) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[((NY - 1) * NG + col) * NV + k] = acc[k];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double tot[NV];
+      const int cg = col < NG ? col : 0;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) tot[k] = red[((NY - 1) * NG + cg) * NV + k];
+#pragma unroll
+      for (int o = 1; o < NY; ++o) {
+        const double* rr = red + ((o - 1) * NG + cg) * NV;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) tot[k] += rr[k];
+      }
+      if (row == 0 && col < NG) {
+        double* out = P.qp + (size_t)q * P.qp_len;
+        const double* uwt = uw_all + s * NU * NU;
+        const int k2 = col / NUT, c2 = col - k2 * NUT;
+        if (col == M * NUT) {
+#pragma unroll
+          for (int a = 0; a < NV; ++a) out[NV * NV + a] = tot[a];  // f
+        } else {
+#pragma unroll
+          for (int a = 0; a < NV; ++a) {  // H = Su' W Su + blkdiag_m(uwt) (S = 1: no G)
+            const double rw = (a / NU == k2) ? uwt[(a % NU) * NU + c2] : 0.0;
+            out[a * NV + k2 * NU + c2] = tot[a] + rw;
+          }
+        }
+      }
+      // the solver's layout in every row (cf. build_rows.hip): lane l < NV
+      // holds row l of H (the column of gather lane (l / NU, l % NU), H is
+      // exactly symmetric) and f[l]
+      constexpr int N = NV;
+      const int rb = lane & ~15;
+      const int lcol = (col < N) ? (col / NU) * NUT + (col % NU) : 0;
+      const double* uwt = uw_all + s * NU * NU;
+      double Hl[N], Fv[N], Gl[1] = {0.0};
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        const double a = __shfl(tot[c], rb + lcol, 64);
+        const double rw = (col < N && c / NU == col / NU) ? uwt[(col % NU) * NU + (c % NU)] : 0.0;
+        Hl[c] = (col < N) ? a + rw : 0.0;
+      }
+      static_for<N>([&](auto A) {
+        constexpr int a = decltype(A)::value;
+        Fv[a] = rbc<M * NUT>(tot[a]);
+      });
+      const double f_l = (col < N) ? sel<N>(Fv, col) : 0.0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // the totals are read before the scratch is written
+      rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
+                                                red + NY * NG * NV + row * N * N);
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     if (row == 0 && col < NG) {
       double tot[NV];
 #pragma unroll
@@ -727,6 +794,40 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
                 dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                               \
     return 0;                                                                          \
   }
+
+// fused build + K iterations on the one-QP-per-wave kernel (S = 1 only: the
+// plan exchange of S > 1 would cross waves)
+#define STEP_WAVE_CASE(NS_, NY_, NU_, M_)                                                \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {   \
+    if (P.lds_per_wave < NY_ * (M_ * 4 + 1) * (NU_ * M_) + 4 * (NU_ * M_) * (NU_ * M_)) \
+      return -1;                                                                         \
+    const size_t lds = sizeof(double) * ((size_t)P.lds_block +                           \
+                                         (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);    \
+    if (P.sv.trace) {                                                                    \
+      auto k_ = cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 2>;                           \
+      if (lds > 64 * 1024)                                                               \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P); \
+    } else {                                                                             \
+      auto k_ = cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 1>;                           \
+      if (lds > 64 * 1024)                                                               \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P); \
+    }                                                                                    \
+    return 0;                                                                            \
+  }
+
+// one workgroup per four QPs (no persistent loop: the fused path is for
+// batches that give fewer waves than the GPU holds)
+int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (P.S != 1) return -1;
+  STEP_WAVE_CASE(11, 3, 4, 2)  // parallel centralized
+  STEP_WAVE_CASE(10, 4, 4, 2)  // serial centralized
+  return -1;
+}
 
 int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
   hipStream_t s = (hipStream_t)stream;

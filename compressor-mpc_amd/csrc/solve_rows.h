@@ -1,0 +1,121 @@
+// The K Jacobi iterations of one QP per 16-lane row (qp_solver_row.h):
+// shared by the row-layout iterate kernel (solve_rows.hip) and the fused
+// build + iterate kernels (build_rows.hip, cmpc_kernels.hip), which hand over
+// H, f and G in registers instead of through HBM.
+//
+// Lane l of the row: Hl = row l of H, f_l = f[l], Gl = row l of G (l < N;
+// zeros in lanes N..15); q = the row's QP (clamped), active = q is a real QP
+// (stores only then); s = its sub-controller, base_lane = lane 0 of the
+// scenario's first row; tsh = this row's N x N LDS scratch.  Every lane of
+// the wave must call it (the plan exchange reads other rows' lanes).
+#pragma once
+#include "cmpc_internal.h"
+#include "qp_solver_row.h"
+
+template <int N, int NU, int NVO, bool TRACE, bool EXT>
+__device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool active, int s, int l,
+                                              int base_lane, const double (&Hl)[N], double f_l,
+                                              const double (&Gl)[NVO > 0 ? NVO : 1], double* tsh) {
+  constexpr int M = N / NU;
+  constexpr int NVOA = NVO > 0 ? NVO : 1;
+  constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
+  const bool own = l < N;
+  const double* cfg = P.cfg + (size_t)s * P.co.len;
+
+  RowQp<N, NU> qp;
+  double uo[NU];
+#pragma unroll
+  for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
+#pragma unroll
+  for (int c = 0; c < NU; ++c) {
+    qp.lb[c] = cfg[P.co.lower + c] - uo[c];
+    qp.ub[c] = cfg[P.co.upper + c] - uo[c];
+    qp.lbA[c] = cfg[P.co.rlower + c];
+    qp.ubA[c] = cfg[P.co.rupper + c];
+  }
+  qp.tolerances();
+  double hr[N];
+  const bool pd = hinv_row<N>(Hl, l, hr, tsh);
+  double hmax = 0.0;
+  {
+    double hd[N];
+    row_gather<N>(sel<N>(Hl, l < N ? l : N - 1), hd);  // H[i][i] from lane i
+#pragma unroll
+    for (int i = 0; i < N; ++i) hmax = fabs(hd[i]) > hmax ? fabs(hd[i]) : hmax;
+  }
+  const double tol_d = TOL_D * (1.0 + hmax);
+
+  uint32_t ws = P.ws[q];
+  double x[N];
+  QpOut o;
+  if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
+    qp_solve_row<false, N, NU>(qp, hr, l, pd, tol_d, f_l, 0u, CMPC_NWSR_MAX, x, o);
+    if (active && l == 0) P.ws[q] = o.ws;
+    return;
+  }
+  double dprev[N];
+#pragma unroll
+  for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+  for (int k = 0; k < P.K; ++k) {
+    {  // fair progress of the SIMD's waves (cf. cmpc_solve_kernel)
+      const int level = 3 - (4 * k) / (P.K > 0 ? P.K : 1);
+      if (level <= 0) __builtin_amdgcn_s_setprio(0);
+      else if (level == 1) __builtin_amdgcn_s_setprio(1);
+      else if (level == 2) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+    }
+    double fk = f_l;
+    if constexpr (NVO > 0) {
+      double dother[NVOA];
+      if constexpr (EXT) {
+        // du_last of DistributedController::GetInput (nerve_center.h:283-285)
+#pragma unroll
+        for (int rk = 0; rk < SM1; ++rk)
+#pragma unroll
+          for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = P.du_other[(size_t)q * NVO + rk * N + mv * NU + c];
+      } else {
+#pragma unroll
+        for (int rk = 0; rk < SM1; ++rk) {
+          const int s2 = rk + (rk >= s ? 1 : 0);
+#pragma unroll
+          for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + 16 * s2 + l, 64);
+        }
+      }
+      // f_k = f + G du_other, entry l (cmpc_solve_kernel's order)
+#pragma unroll
+      for (int c = 0; c < NVOA; ++c) fk = fk + Gl[c] * dother[c];
+    }
+    qp_solve_row<TRACE, N, NU>(qp, hr, l, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
+    ws = o.ws;
+#pragma unroll
+    for (int a = 0; a < N; ++a) dprev[a] = x[a];
+    if (TRACE && active && l == 0 && P.trace) {
+      uint32_t* tr = reinterpret_cast<uint32_t*>(P.trace + ((size_t)q * P.K + k) * 16);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) tr[t] = o.tr[t];
+      P.ntrace[(size_t)q * P.K + k] = o.ntrace;
+    }
+  }
+  if (!active) return;
+  if (l == 0) {
+    P.ws[q] = ws;
+    if (P.K > 0) {
+      P.status[q] = o.status;
+      P.nwsr[q] = o.nchg;
+    }
+  }
+  if (own) {
+    const double v = sel<N>(dprev, l);
+    P.du[(size_t)q * N + l] = v;
+    P.du_old[(size_t)q * N + l] = v;
+  }
+  if ((P.flags & CMPC_APPLY_MOVE) && l < NU) {
+    P.u_old[(size_t)q * P.nu_tot + l] = sel<NU>(uo, l) + sel<N>(dprev, l);
+  }
+}

@@ -166,6 +166,30 @@ int cmpc_set_build_variant(cmpc_ctx* ctx, int variant);
 /* The build kernel the last cmpc_build launched (CMPC_BUILD_WAVE or
  * CMPC_BUILD_ROWS), 0 before the first build, <0 on a null context. */
 int cmpc_last_build_kernel(cmpc_ctx* ctx);
+/* Solve-kernel selection for cmpc_iterate / cmpc_init_warmstart /
+ * cmpc_get_input (the same results bit for bit):
+ * CMPC_SOLVE_LANE one QP per lane (large batches); CMPC_SOLVE_ROWS one QP per
+ * 16-lane DPP row, its H^-1 and matrix-vector products spread over the row
+ * (batches that leave most SIMDs idle; needs S | 4); CMPC_SOLVE_AUTO
+ * (default) rows below CMPC_SOLVE_ROWS_MAX_QP QPs where available. */
+#define CMPC_SOLVE_AUTO 0
+#define CMPC_SOLVE_LANE 1
+#define CMPC_SOLVE_ROWS 2
+int cmpc_set_solve_variant(cmpc_ctx* ctx, int variant);
+/* The solve kernel the last iterate / init / get-input launched. */
+int cmpc_last_solve_kernel(cmpc_ctx* ctx);
+/* cmpc_step as one launch (the build kernel runs the K Jacobi iterations of
+ * the QPs it built, H, f, G handed over in registers; the same results bit
+ * for bit as cmpc_build + cmpc_iterate with the row solve kernel):
+ * CMPC_STEP_SPLIT two launches; CMPC_STEP_FUSED one (an error where no fused
+ * kernel exists for the dimensions); CMPC_STEP_AUTO (default) fused below
+ * CMPC_SOLVE_ROWS_MAX_QP QPs where available. */
+#define CMPC_STEP_AUTO 0
+#define CMPC_STEP_SPLIT 1
+#define CMPC_STEP_FUSED 2
+int cmpc_set_step_variant(cmpc_ctx* ctx, int variant);
+/* 1 if the last cmpc_step ran fused, 0 if split, <0 on a null context. */
+int cmpc_last_step_fused(cmpc_ctx* ctx);
 /* Diagnostic (no GPU needed): the row kernel's LDS layout for *dims as
  * cmpc_build chooses it.  Writes the bank-conflict model's extra LDS cycles
  * per wave-step of the horizon loop (wave 0) for the packed layout (regions
@@ -197,7 +221,8 @@ int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
 #define CMPC_KERNEL_PRODUCE 2         /* cmpc_produce_lin; cmpc_observe_step (a posteriori + per-QP producer, one kernel) */
 #define CMPC_KERNEL_OBSERVE_POST 3    /* no launches since the a posteriori update runs in the producer (kept for the numbering) */
 #define CMPC_KERNEL_OBSERVE_PRIOR 4   /* cmpc_observe_apply */
-#define CMPC_KERNEL_COUNT 5
+#define CMPC_KERNEL_STEP 5            /* cmpc_step as one fused build + K-iteration launch */
+#define CMPC_KERNEL_COUNT 6
 #define CMPC_TIME_ONLY(kernel) (2 << (kernel))
 int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
 int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,

@@ -1,0 +1,160 @@
+"""Small-batch kernels (SURVEY configs 2 and 5, B = 1): the row-layout solve
+kernel (one QP per 16-lane DPP row, csrc/solve_rows.hip) against the
+one-QP-per-lane kernel, bit for bit, on the same QPs and states: plans,
+statuses, working-set change counts, working sets and the change sequence of
+every Jacobi iteration, over init + several closed-loop steps with the first
+move applied.  (The step-parity tests of test_gpu_parity.py, B = 96, run the
+row kernel against the oracle through CMPC_SOLVE_AUTO.)"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+import cmpc
+from cmpc.configs import reference_setup
+from cmpc.synthetic import synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # plant, controller, p, m, K, B scenarios
+    ("par", "coop", 20, 2, 9, 512),
+    ("par", "coop", 20, 2, 9, 13),
+    ("par", "coop", 50, 2, 9, 4096),
+    ("par", "ncoop", 50, 2, 9, 512),
+    ("par", "cent", 200, 2, 1, 1024),
+    ("ser", "cent", 100, 2, 3, 256),
+    ("ser", "coop", 50, 2, 9, 256),
+    ("par", "coop", 50, 1, 9, 256),
+    ("par", "coop", 30, 3, 9, 256),
+]
+
+
+def _tight(arr, f):
+    """Tighter input and rate bounds: more active constraints per QP."""
+    return dataclasses.replace(arr, lower=arr.lower * f, upper=arr.upper * f,
+                               rate_lower=arr.rate_lower * f, rate_upper=arr.rate_upper * f)
+
+
+def _run(cfg, arr, lin, u, du, ws, K, variant, steps=3):
+    out = []
+    with cmpc.Context(cfg, lin.shape[0] // cfg.S) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u, du, ws)
+        ctx.upload_lin(lin)
+        ctx.set_solve_variant(variant)
+        for step in range(steps):
+            flags = cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE
+            ctx.build()
+            if step == 0:
+                ctx.init_warmstart()
+            ctx.iterate(K, flags)
+            assert ctx.last_solve_kernel() == variant
+            d, st, nw = ctx.download()
+            tr, ntr = ctx.download_trace(K)
+            out.append((d, st, nw, *ctx.get_state(), tr, ntr))
+    return out
+
+
+@pytest.mark.parametrize("plant,ctype,p,m,K,B", CASES)
+@pytest.mark.parametrize("tight", [1.0, 0.3])
+def test_gpu_row_solver_equals_lane_solver(plant, ctype, p, m, K, B, tight):
+    cfg = cmpc.reference_config(plant, ctype, p=p, m=m)
+    arr = _tight(cmpc.controller_arrays(cfg, reference_setup(plant, ctype)), tight)
+    lin, u, du, ws = synthetic_batch(cfg, B, seed=40 + p + m, n_distinct=min(B, 512))
+    lane = _run(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_SOLVE_LANE)
+    rows = _run(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_SOLVE_ROWS)
+    names = ("du", "status", "nwsr", "u_old", "du_old", "ws", "trace", "ntrace")
+    for step, (a, b) in enumerate(zip(lane, rows)):
+        for name, x, y in zip(names, a, b):
+            assert np.array_equal(x, y), (step, name, np.flatnonzero((x != y).reshape(len(x), -1).any(1))[:8])
+    st, ntr = lane[-1][1], lane[-1][-1]
+    print(f"{plant}-{ctype} p={p} m={m} tight={tight}: ok {np.mean(st == 0):.3f}, "
+          f"active {np.mean(lane[-1][5] != 0):.3f}, changes/QP {ntr.sum() / len(st):.3f}")
+
+
+def test_gpu_row_solver_failure_statuses_equal_lane_solver():
+    """Non-finite records (a NaN gradient -> NONFINITE, a NaN Hessian ->
+    NOT_PD): the same status and the zero move from both kernels."""
+    cfg = cmpc.reference_config("par", "coop", p=20)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    B = 64
+    lin, u, du, ws = synthetic_batch(cfg, B, seed=9, n_distinct=64)
+    L = cmpc.layout_of(cmpc.CmpcDims.from_config(cfg, B))
+    lin = lin.copy()
+    lin[3, L.off_y] = np.nan          # y_prev: f only
+    lin[10, L.off_A] = np.nan         # A: H and f
+    lin[21, L.off_x + 5] = np.inf     # a delay state: f only
+    res = [_run(cfg, arr, lin, u, du, ws, 9, v, steps=2) for v in (cmpc.CMPC_SOLVE_LANE, cmpc.CMPC_SOLVE_ROWS)]
+    for a, b in zip(*res):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    st = res[0][-1][1]
+    assert st[3] != cmpc.CMPC_QP_OK and st[10] != cmpc.CMPC_QP_OK and st[21] != cmpc.CMPC_QP_OK
+    assert (st == cmpc.CMPC_QP_OK).mean() > 0.9
+
+
+def test_gpu_solve_auto_picks_rows_for_small_batches():
+    cfg = cmpc.reference_config("par", "coop", p=20)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    for B, expect in ((16, cmpc.CMPC_SOLVE_ROWS), (65536, cmpc.CMPC_SOLVE_LANE)):
+        lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
+        with cmpc.Context(cfg, B) as ctx:
+            ctx.configure(arr)
+            ctx.set_state(u, du, ws)
+            ctx.upload_lin(lin)
+            ctx.build()
+            ctx.init_warmstart()
+            ctx.iterate(1)
+            assert ctx.last_solve_kernel() == expect, B
+
+
+FUSED_CASES = [  # plant, controller, p, K, B scenarios (the kernel AUTO fuses on)
+    ("par", "coop", 20, 9, 4096),     # SURVEY config 2: the row build kernel
+    ("par", "coop", 20, 9, 13),
+    ("par", "coop", 50, 9, 1),        # B = 1, the reference's own call pattern
+    ("par", "ncoop", 50, 9, 64),
+    ("par", "cent", 200, 1, 1024),    # SURVEY config 5: the one-QP-per-wave kernel
+    ("ser", "cent", 100, 1, 1),       # SURVEY config 1 at B = 1
+    ("ser", "cent", 100, 3, 512),
+    ("ser", "coop", 50, 9, 64),
+]
+
+
+def _run_step(cfg, arr, lin, u, du, ws, K, variant, steps=3):
+    out = []
+    with cmpc.Context(cfg, lin.shape[0] // cfg.S) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u, du, ws)
+        ctx.upload_lin(lin)
+        ctx.build()
+        ctx.init_warmstart()
+        ctx.set_step_variant(variant)
+        if variant == cmpc.CMPC_STEP_SPLIT:
+            ctx.set_solve_variant(cmpc.CMPC_SOLVE_ROWS)
+        for step in range(steps):
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE)
+            assert ctx.last_step_fused() == (variant == cmpc.CMPC_STEP_FUSED)
+            d, st, nw = ctx.download()
+            tr, ntr = ctx.download_trace(K)
+            out.append((d, st, nw, *ctx.get_state(), tr, ntr, *ctx.download_qp()))
+    return out
+
+
+@pytest.mark.parametrize("plant,ctype,p,K,B", FUSED_CASES)
+def test_gpu_fused_step_equals_split_step(plant, ctype, p, K, B):
+    """cmpc_step as one launch (the build kernel solves its own QPs) against
+    cmpc_build + cmpc_iterate: the QPs (H, f, G), plans, statuses, working
+    sets, states and change sequences of three steps, bit for bit."""
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arr = _tight(cmpc.controller_arrays(cfg, reference_setup(plant, ctype)), 0.5)
+    lin, u, du, ws = synthetic_batch(cfg, B, seed=70 + p, n_distinct=min(B, 512))
+    split = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_SPLIT)
+    fused = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_FUSED)
+    names = ("du", "status", "nwsr", "u_old", "du_old", "ws", "trace", "ntrace", "H", "f", "G")
+    for step, (a, b) in enumerate(zip(split, fused)):
+        for name, x, y in zip(names, a, b):
+            if x is None:
+                continue
+            assert np.array_equal(x, y), (step, name)
+    print(f"{plant}-{ctype} p={p} B={B}: ok {np.mean(split[-1][1] == 0):.3f}, "
+          f"changes/QP {split[-1][7].sum() / len(split[-1][1]):.3f}")

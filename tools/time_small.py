@@ -18,6 +18,8 @@ CONFIGS = {  # name: (plant, controller, p, B scenarios, K)
     "b1": ("par", "coop", 50, 1, 9),
     "c1b1": ("ser", "cent", 100, 1, 1),
     "c3": ("par", "ncoop", 50, 65536, 1),
+    "c1": ("ser", "cent", 100, 65536, 1),
+    "head": ("par", "coop", 50, 65536, 9),
 }
 REPS = int(os.environ.get("CMPC_TS_REPS", "50"))
 VARS = [("wave", cmpc.CMPC_BUILD_WAVE), ("rows", cmpc.CMPC_BUILD_ROWS), ("auto", cmpc.CMPC_BUILD_AUTO)]
@@ -61,26 +63,52 @@ for name in (sys.argv[1:] or ["c5", "c2", "b1"]):
             res.append(f"{vn} {ms / n * 1e3:7.2f}")
         ctx.set_build_variant(cmpc.CMPC_BUILD_AUTO)
         its = []
-        for k in (0, 1, K):
-            ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
+        for sv, sn in ((getattr(cmpc, "CMPC_SOLVE_LANE", None), "lane"), (getattr(cmpc, "CMPC_SOLVE_ROWS", None), "rows")):
+            if sv is None:
+                continue
+            ctx.set_solve_variant(sv)
+            for k in (0, 1, K):
+                ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
+                for _ in range(REPS):
+                    ctx.iterate(k)
+                ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
+                ctx.enable_timing(False)
+                its.append(f"{sn} K={k} {ms / n * 1e3:6.2f}")
+        if hasattr(cmpc, "CMPC_SOLVE_AUTO"):
+            ctx.set_solve_variant(cmpc.CMPC_SOLVE_AUTO)
+        steps = []
+        variants = [("split", getattr(cmpc, "CMPC_STEP_SPLIT", None)), ("fused", getattr(cmpc, "CMPC_STEP_FUSED", None)),
+                    ("auto", getattr(cmpc, "CMPC_STEP_AUTO", None))]
+        for vn, v in variants:
+            if v is None and vn != "auto":
+                continue
+            try:
+                if v is not None:
+                    ctx.set_step_variant(v)
+                ctx.step(K)
+                ctx.synchronize()
+            except Exception:  # noqa: BLE001
+                steps.append(f"{vn} n/a")
+                continue
+            settle(ctx, K, 0.1)
+            t0 = time.perf_counter()
             for _ in range(REPS):
-                ctx.iterate(k)
-            ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
-            ctx.enable_timing(False)
-            its.append(f"K={k} {ms / n * 1e3:6.2f}")
-        settle(ctx, K, 0.1)
-        t0 = time.perf_counter()
-        for _ in range(REPS):
-            ctx.build()
-            ctx.iterate(K)
-        ctx.synchronize()
-        t_bb = (time.perf_counter() - t0) / REPS
-        t0 = time.perf_counter()
-        for _ in range(REPS):
-            ctx.build()
-            ctx.iterate(K)
+                ctx.step(K)
             ctx.synchronize()
-        t_sync = (time.perf_counter() - t0) / REPS
+            t_bb = (time.perf_counter() - t0) / REPS
+            t0 = time.perf_counter()
+            for _ in range(REPS):
+                ctx.step(K)
+                ctx.synchronize()
+            t_sync = (time.perf_counter() - t0) / REPS
+            kern = ""
+            if vn == "fused":
+                ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_STEP,))
+                for _ in range(REPS):
+                    ctx.step(K)
+                ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_STEP)
+                ctx.enable_timing(False)
+                kern = f" kernel {ms / n * 1e3:.2f}"
+            steps.append(f"{vn} {t_bb * 1e6:.1f}/{t_sync * 1e6:.1f}{kern}")
     print(f"{name:5s} {plant}-{ctype} p={p} B={B} K={K}  build us: {', '.join(res)} | iterate us: "
-          f"{', '.join(its)} | step us back-to-back {t_bb * 1e6:.1f}, synchronised {t_sync * 1e6:.1f}",
-          flush=True)
+          f"{', '.join(its)} | step us back-to-back/synchronised: {'; '.join(steps)}", flush=True)
