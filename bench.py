@@ -81,41 +81,52 @@ def build_bytes(cfg, L) -> float:
     return 8.0 * (rec + nu_tot + out)
 
 
-# sources that determine the build kernel's code (and so its HBM traffic)
-BUILD_SOURCES = ("compressor-mpc_amd/csrc/build_rows.hip", "compressor-mpc_amd/csrc/rows_blocks.inc",
-                 "compressor-mpc_amd/csrc/rows_layout.cpp", "compressor-mpc_amd/csrc/cmpc_internal.h",
-                 "compressor-mpc_amd/csrc/Makefile")
+# the bench's build-kernel instantiation (cmpc_build_rows_kernel<NS=11, NY=3,
+# NUT=4, NU=2, M=2, ND=2, WPG=4, RING=false, WPE=3, FUSE=0>)
+BENCH_KERNEL_SYMBOL = "cmpc_build_rows_kernelILi11ELi3ELi4ELi2ELi2ELi2ELi4ELb0ELi3ELi0EE"
 
 
-def build_source_hash() -> str:
-    """sha256 over the build kernel's sources: ties a PMC traffic figure
-    under profiles/ to the code it was measured on."""
-    h = hashlib.sha256()
-    for rel in BUILD_SOURCES:
-        with open(os.path.join(ROOT, rel), "rb") as fh:
-            h.update(rel.encode() + b"\0" + fh.read())
-    return h.hexdigest()[:16]
+def bench_kernel_code_hash():
+    """sha256 of the bench build kernel's gfx950 machine code in the loaded
+    library (tools/kernel_hash.py): ties a PMC traffic figure under profiles/
+    to the code it was measured on; other instantiations, comments and the
+    solve kernels do not change it."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_hash
+    from cmpc._abi import LIB_PATH
+    blob = open(LIB_PATH, "rb").read()
+    for co in kernel_hash.code_objects(blob):
+        r = kernel_hash.kernel_bytes(co, BENCH_KERNEL_SYMBOL)
+        if r:
+            return hashlib.sha256(r[1]).hexdigest()[:16]
+    return None
 
 
 def pmc_traffic(B: int, kernel: str):
     """(bytes per launch, provenance) from profiles/pmc_build_coop_p50.json
-    when it was measured on this batch, this kernel and these sources;
-    (None, reason) otherwise."""
+    when it was measured on this batch, this kernel and this kernel's machine
+    code; (None, reason) otherwise."""
     path = os.path.join(ROOT, "profiles", "pmc_build_coop_p50.json")
     try:
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None, {"file": "profiles/pmc_build_coop_p50.json", "status": "missing"}
+    try:
+        cur = bench_kernel_code_hash()
+    except Exception as e:  # noqa: BLE001 -- reported, never required
+        cur = None
+        log(f"kernel code hash failed: {e}")
     prov = {"file": "profiles/pmc_build_coop_p50.json", "pmc_source": rec.get("source"),
-            "round": rec.get("round"), "measured_source_hash": rec.get("build_source_hash"),
-            "current_source_hash": build_source_hash()}
+            "round": rec.get("round"), "measured_code_hash": rec.get("build_kernel_code_hash"),
+            "current_code_hash": cur,
+            "hash_of": "gfx950 machine code of " + BENCH_KERNEL_SYMBOL + " in the loaded libcmpc.so"}
     if rec.get("batch") != B or rec.get("kernel") != kernel:
         prov["status"] = "not this workload"
         return None, prov
-    if rec.get("build_source_hash") != prov["current_source_hash"]:
-        prov["status"] = "stale: measured on other build-kernel sources"
+    if cur is None or rec.get("build_kernel_code_hash") != cur:
+        prov["status"] = "stale: measured on another build of the bench kernel"
         return None, prov
-    prov["status"] = "measured on these sources (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes)"
+    prov["status"] = "measured on this machine code (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes)"
     return rec.get("hbm_bytes_per_launch"), prov
 
 
@@ -208,6 +219,140 @@ def cpu_baseline(cfg, arrays, lin, u_old, K, target_s):
     }
 
 
+def traced_changes(ctx, K, bind, steps):
+    """Working-set changes per step summed over all K Jacobi iterations and all
+    QPs (the trace counts of CMPC_TRACE), over `steps` steps bound by bind(i)
+    (untimed; the caller restores the states afterwards)."""
+    import cmpc
+    tot = []
+    for i in steps:
+        bind(i)
+        ctx.step(K, cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE)
+        _, ntr = ctx.download_trace(K)
+        tot.append(int(ntr.sum()))
+    return float(np.mean(tot)), tot
+
+
+def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2, seed=4000):
+    """One SURVEY §8(d) configuration on this GPU: NB resident batches of B
+    scenarios, each with its own controller state, step i on batch i % NB
+    (build + K Jacobi iterations, first move applied: cmpc_step, fused into
+    one launch where CMPC_STEP_AUTO picks that); then the build kernel alone
+    with events for its roofline fraction."""
+    import torch
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.synthetic import synthetic_batch
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    arrays = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
+    dev = f"cuda:{local}"
+    recs, sts = [], []
+    for b in range(NB):
+        lin, u, du, w = synthetic_batch(cfg, B, seed=seed + 31 * b, n_distinct=min(B, 1024))
+        recs.append(torch.from_numpy(lin).to(dev))
+        sts.append(tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (u, du, w.view(np.int32))))
+    ctx = cmpc.Context(cfg, B, device=local)
+    try:
+        ctx.configure(arrays)
+
+        def bind(i):
+            st_ = sts[i % NB]
+            ctx.bind_lin(recs[i % NB].data_ptr())
+            ctx.bind_state(st_[0].data_ptr(), st_[1].data_ptr(), st_[2].data_ptr())
+
+        for b in range(NB):
+            bind(b)
+            ctx.build()
+            ctx.init_warmstart()
+        snap = [tuple(a.clone() for a in st_) for st_ in sts]
+        i = 0
+        t_end = time.perf_counter() + settle_seconds
+        while time.perf_counter() < t_end or i < 8:
+            bind(i)
+            ctx.step(K, 0)
+            i += 1
+            if i % 16 == 0:
+                ctx.synchronize()
+        ctx.synchronize()
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            bind(i + k)
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+        ctx.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        fused = ctx.last_step_fused()
+        # one step at a time (host waits for each): the latency view
+        t0 = time.perf_counter()
+        for k in range(steps):
+            bind(i + k)
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+            ctx.synchronize()
+        dt_sync = (time.perf_counter() - t0) / steps
+        # device time of the step's kernels (events), then the build alone
+        ctx.enable_timing(True)
+        for k in range(steps):
+            bind(i + k)
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+        kt = {}
+        for kn, kid in (("build", cmpc.CMPC_KERNEL_BUILD), ("iterate", cmpc.CMPC_KERNEL_ITERATE),
+                        ("fused_step", cmpc.CMPC_KERNEL_STEP)):
+            ms, n = ctx.kernel_time(kid)
+            if n:
+                kt[kn] = ms / n
+        ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+        for k in range(steps):
+            bind(i + k)
+            ctx.build()
+        bms, bn = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+        ctx.enable_timing(False)
+        bkern = "cmpc_build_rows_kernel" if ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS else "cmpc_build_kernel"
+        L = ctx.layout
+        changes, _ = traced_changes(ctx, K, bind, range(i, i + NB))
+        for st_, sn in zip(sts, snap):
+            for a, a0 in zip(st_, sn):
+                a.copy_(a0)
+        _, st, _ = ctx.download()
+    finally:
+        ctx.close()
+    f_b = build_flops(cfg, L.naug, L.nd)
+    b_s = bms / max(bn, 1) / 1e3
+    return {"config": name, "plant": plant, "controller": ctype, "p": p, "B": B, "qp": B * cfg.S, "K": K,
+            "qp_solves_per_s": B * cfg.S * K / dt, "ms_per_step": dt * 1e3,
+            "ms_per_step_synchronised": dt_sync * 1e3, "step_fused": fused, "kernels_ms": kt,
+            "build_kernel": bkern, "build_ms": b_s * 1e3,
+            "build_roofline": {"flops_per_qp": f_b, "achieved_tflops": B * cfg.S * f_b / b_s / 1e12,
+                               "frac": B * cfg.S * f_b / b_s / 1e12 / FP64_PEAK_TFLOPS,
+                               "peak": FP64_PEAK_TFLOPS, "bound": "fp64-valu"},
+            "working_set_changes_per_step": changes, "qp_status_ok_fraction": float((st == 0).mean())}
+
+
+def cpp_step_latency(plant, ctype, p, steps=400):
+    """B = 1 step latency through the C++ adapter (tests/cpp/nerve_center_latency:
+    NerveCenter::GetNextInput with the device observer, host clock per call)."""
+    import subprocess
+    import tempfile
+    from cmpc.configs import reference_setup
+    exe = os.path.join(ROOT, "tests", "cpp", "nerve_center_latency")
+    if not os.path.exists(exe):
+        return {"error": "tests/cpp/nerve_center_latency not built (make -C tests/cpp)"}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, f"setup-{ctype}-{plant}")
+        with open(path, "w") as fh:
+            fh.write(reference_setup(plant, ctype).text())
+        r = subprocess.run([exe, path, plant, ctype, str(p), str(steps)], capture_output=True, text=True,
+                           timeout=120)
+    if r.returncode:
+        return {"error": r.stderr.strip()[-300:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out.update({"plant": plant, "controller": ctype, "p": p, "B": 1,
+                "note": "NerveCenter::GetNextInput (observer a posteriori + linearisation, build, K Jacobi "
+                        "iterations, download, a-priori update) through include/cmpc/nerve_center.hpp, one "
+                        "scenario, host clock per call; the reference recorded 371.3 us (cent-ser) and "
+                        "900.4 us (coop-par K = 9) per step at p = 100 on its CPU"})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +372,8 @@ def main():
                     help="only the metric's steps (no K = 1, closed-loop, coupled or CPU sections): "
                          "profiler runs, so that every build launch in the trace is a headline one")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the SURVEY-config section (configs 1, 2, 3, 5 on this GPU)")
     ap.add_argument("--coupled-batch", type=int, default=4096, help="config-4 scenarios per GPU")
     ap.add_argument("--coupled-tiles", type=int, default=1,
                     help="config-4 scenario tiles per GPU, each on its own stream: a tile's "
@@ -363,6 +510,53 @@ def main():
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     ctx.enable_timing(False)
     restore()
+    # working-set changes of the timed workload, summed over the K Jacobi
+    # iterations and all QPs of a step (CMPC_TRACE counts, untimed pass over
+    # one rotation of the batches)
+    ws_changes, _ = traced_changes(ctx, K, bind, range(first, first + NB))
+    restore()
+
+    # harder_qp: every state set meets other records at each of its steps
+    # (step i: state i % NB, records (i + i // NB) % NB), so each QP's warm
+    # start comes from another QP's solution and the active sets move
+    harder = None
+    if not args.headline_only:
+        def bind_h(i):
+            st_ = states[i % NB]
+            ctx.bind_lin(batches[(i + i // NB) % NB].data_ptr())
+            ctx.bind_state(st_[0].data_ptr(), st_[1].data_ptr(), st_[2].data_ptr())
+        try:
+            for i in range(2 * NB):
+                bind_h(i)
+                ctx.step(K, 0)
+            ctx.synchronize()
+            restore()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                bind_h(first + i)
+                ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+            ctx.synchronize()
+            t_h = (time.perf_counter() - t0) / args.steps
+            restore()
+            ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
+            for i in range(args.steps):
+                bind_h(first + i)
+                ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+            ctx.synchronize()
+            ims_h, nih = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
+            ctx.enable_timing(False)
+            restore()
+            ch_h, _ = traced_changes(ctx, K, bind_h, range(first, first + NB))
+            restore()
+            harder = {"ms_per_step": t_h * 1e3, "qp_solves_per_s_per_gpu": B * S * K / t_h,
+                      "iterate_ms": ims_h / max(nih, 1), "working_set_changes_per_step": ch_h,
+                      "note": "step i binds state set i % NB to records (i + i // NB) % NB: every warm "
+                              "start comes from the solution of another QP (the reference's hotstart "
+                              "after its QP changed, libs/mpc_qp_solver.cc:62-64)"}
+        except Exception as e:  # reported, never required
+            log(f"harder_qp variant failed: {e}")
+        finally:
+            restore()
     # the sections below run on the context's own state buffers
     ctx.bind_state()
     ctx.bind_lin(0)
@@ -567,6 +761,27 @@ def main():
         # SURVEY config 4 (sub-controllers sharded over the ranks, RCCL all-gather
         # of the plans once per Jacobi iteration), beside the metric: every rank
         # takes part, so at world N it times the exchange over xGMI
+    # SURVEY §8(d) / BASELINE.json configs beside the metric, this GPU:
+    # 1 (cent-ser p = 100) as the reference's B = 1 call through the C++
+    # adapter, 2, 3 and 5 at their batch sizes; 4 is the `coupled` section
+    configs = None
+    if not args.no_configs and not args.headline_only and world == 1:
+        configs = {}
+        for key, (pl, ct, p_, B_, K_) in {"2": ("par", "coop", 20, 4096, 9),
+                                         "3": ("par", "ncoop", 50, 65536, 1),
+                                         "5": ("par", "cent", 200, 1024, 1)}.items():
+            try:
+                configs[key] = time_config(key, pl, ct, p_, B_, K_, local, args.settle_seconds,
+                                           max(20, args.steps))
+            except Exception as e:  # reported, never required
+                log(f"config {key} failed: {e}")
+                configs[key] = {"error": str(e)[:300]}
+        for key, (pl, ct, p_) in {"1": ("ser", "cent", 100), "b1_coop_par": ("par", "coop", 50)}.items():
+            try:
+                configs[key] = cpp_step_latency(pl, ct, p_)
+            except Exception as e:  # reported, never required
+                log(f"config {key} failed: {e}")
+                configs[key] = {"error": str(e)[:300]}
     coupled, rc, el_c = None, None, float("inf")
     if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench
@@ -598,9 +813,12 @@ def main():
                     "coupled iteration), first move applied; with tiles > 1 the scenarios run as "
                     "that many tiles on their own streams, each tile's all-gather overlapping "
                     "another tile's iteration (cmpc.coupled.CoupledPipeline; slower at world 1, "
-                    "DESIGN.md section 8); per-GPU work grows with S_total "
-                    "(G_ext is nV x (S_total - 1) nV per QP); gather_ms (summed over the tiles) "
-                    "from events in a separate pass"})
+                    "DESIGN.md section 8); gather_ms (summed over the tiles) from events in a "
+                    "separate pass",
+            "scaling_note": ("not constant work per GPU: S_total = 8 x world, so each QP's f_k update "
+                             "reads nV x (S_total - 1) nV coupling entries and the gathered plans grow "
+                             "with world; a SCALE curve of this section is weak scaling in scenarios "
+                             "per GPU with per-QP work growing linearly in world size")})
 
     ok_frac = float((st == 0).mean())
     active_frac = float((ws_now != 0).mean())
@@ -641,9 +859,9 @@ def main():
             "parallelism": f"scenario-sharded replicas x{world} (no data-path collective)",
         },
         "roofline": {
-            "bound": "mfma",
+            "bound": "fp64-valu",
             "pipe": "fp64 VALU (v_fmac_f64_dpp); MI355X FP64 vector peak = FP64 matrix peak",
-            "kernel": build_kernel + "<NS=11,NY=3,NUT=4,NU=2,M=2,ND=2>",
+            "kernel": build_kernel + "<NS=11,NY=3,NUT=4,NU=2,M=2,ND=2,WPG=4,RING=0,WPE=3>",
             "achieved": achieved_tf,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
@@ -682,6 +900,11 @@ def main():
         "qp_active_constraint_fraction": active_frac,
         "u_old_max_drift_over_timed_steps": u_drift,
         "mean_working_set_changes_last_solve": mean_chg,
+        "working_set_changes_per_step": ws_changes,
+        "working_set_changes_note": ("summed over all K Jacobi iterations and all QPs of one timed step "
+                                     "(CMPC_TRACE counts; untimed pass over one batch rotation)"),
+        "harder_qp": harder,
+        "configs": configs,
         "closed_loop_device_resident": closed,
         "coupled": coupled,
     }

@@ -114,6 +114,26 @@ class SetupFile:
             "yref", "uwt", "ywt", "constraints-lower", "constraints-upper",
             "constraints-rate-lower", "constraints-rate-upper", "simulation")
 
+    def text(self, folder: str = "parallel", output: str = "out.dat") -> str:
+        """The setup-file layout parse() and the C++ reader (cmpc::SetupFile,
+        read_files.h:13-81) read: key line, value lines, blank line."""
+        def mat(vals):
+            n = int(round(len(vals) ** 0.5))
+            return "\n".join("\t".join("%.17g" % v for v in vals[r * n:(r + 1) * n]) for r in range(n))
+        parts = [("n-iterations", str(self.n_iterations)),
+                 ("n-timing-iterations", str(self.n_timing_iterations)),
+                 ("folder-name", folder), ("output-filename", output),
+                 ("yref", " ".join("%.17g" % v for v in self.yref)),
+                 ("uwt", mat(self.uwt)), ("ywt", "\n\n".join(mat(b) for b in self.ywt)),
+                 ("constraints-lower", "\t".join("%.17g" % v for v in self.constraints_lower)),
+                 ("constraints-upper", "\t".join("%.17g" % v for v in self.constraints_upper)),
+                 ("constraints-rate-lower", "\t".join("%.17g" % v for v in self.rate_lower)),
+                 ("constraints-rate-upper", "\t".join("%.17g" % v for v in self.rate_upper))]
+        if self.segments:
+            parts.append(("simulation", "\n\n".join(" ".join("%.17g" % v for v in d) + "\n%.17g" % te
+                                                      for d, te in self.segments)))
+        return "".join(f"{k}\n{v}\n\n" for k, v in parts)
+
     @classmethod
     def parse(cls, text: str, cfg: ControllerConfig) -> "SetupFile":
         blocks, key = {}, None

@@ -180,6 +180,7 @@ struct cmpc_ctx {
   int solve_variant = CMPC_SOLVE_AUTO;  // cmpc_set_solve_variant
   int last_solve = 0;                   // kernel launched by the last solve
   int step_variant = CMPC_STEP_AUTO;    // cmpc_set_step_variant
+  int cus = 0;                          // compute units of the device (0: not yet queried)
   int last_step_fused = 0;
   // timing
   int timing = 0;  // bit k: kernel k (CMPC_KERNEL_*) is timed
@@ -1499,8 +1500,14 @@ int cmpc_last_solve_kernel(cmpc_ctx* c) {
 // the iterate / init / get-input launch through the selected solve kernel
 static int launch_solve(cmpc_ctx* c, const SolveParams& P, const char* who) {
   const int nV = c->L.nV, nu = c->d.nu, nVo = c->L.nVo;
+  // AUTO: the row kernel for small batches of nV >= 6 QPs (centralized: the
+  // lane kernel's nV = 8 solve is one long dependency chain per lane, 25 us
+  // for one solve of 1 024 QPs against 18 us in rows, tools/time_small.py);
+  // at nV = 4 the lane kernel is faster at every batch size (K = 9 on 8 192
+  // QPs: 15.3 vs 21.2 us: the row gathers cost more than the 4 x 4 products
+  // they spread)
   const bool want_rows = c->solve_variant == CMPC_SOLVE_ROWS ||
-                         (c->solve_variant == CMPC_SOLVE_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP);
+                         (c->solve_variant == CMPC_SOLVE_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP && nV >= 6);
   if (want_rows && cmpc_launch_solve_rows(P, nV, nu, nVo, c->stream) == 0) {
     c->last_solve = CMPC_SOLVE_ROWS;
     return 0;
@@ -1695,8 +1702,17 @@ int cmpc_last_step_fused(cmpc_ctx* c) {
 int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   if (!c) return fail("null context");
   if (K < 0) return fail("K must be >= 0");
+  // AUTO fuses small batches where the fused kernel is the build kernel AUTO
+  // would pick anyway: the one-QP-per-wave kernel for centralized batches
+  // under one row group per SIMD (SURVEY config 5: 43.9 vs 46.1 us per step),
+  // the row kernel from one row group per SIMD up (config 2: 36.0 vs
+  // 37.8 us); a coop batch under 4 096 QPs stays split (wave build + lane
+  // solve: B = 1 28.2 vs 33.1 us fused on the row kernel)
+  if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const bool rows_fill_ = (c->nqp + 3) / 4 >= 4 * (c->cus > 0 ? c->cus : 256);
+  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && (c->d.S == 1 || rows_fill_);
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
-                    (c->step_variant == CMPC_STEP_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP &&
+                    (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);
   if (want && K > 0 && c->L.nuo == (c->d.S - 1) * c->d.nu) {
     if (ensure_cfg(c)) return -1;

@@ -93,19 +93,27 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
     assert (st == cmpc.CMPC_QP_OK).mean() > 0.9
 
 
-def test_gpu_solve_auto_picks_rows_for_small_batches():
-    cfg = cmpc.reference_config("par", "coop", p=20)
-    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
-    for B, expect in ((16, cmpc.CMPC_SOLVE_ROWS), (65536, cmpc.CMPC_SOLVE_LANE)):
-        lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
-        with cmpc.Context(cfg, B) as ctx:
-            ctx.configure(arr)
-            ctx.set_state(u, du, ws)
-            ctx.upload_lin(lin)
-            ctx.build()
-            ctx.init_warmstart()
-            ctx.iterate(1)
-            assert ctx.last_solve_kernel() == expect, B
+@pytest.mark.parametrize("ctype,B,solve,fused", [
+    ("cent", 16, cmpc.CMPC_SOLVE_ROWS, True), ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
+    ("coop", 1, cmpc.CMPC_SOLVE_LANE, False), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, True),
+    ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
+def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
+    """CMPC_SOLVE_AUTO: the row solve kernel for small nV = 8 batches only;
+    CMPC_STEP_AUTO: cmpc_step fused for small centralized batches and for
+    coop batches of one row group per SIMD up to 16 384 QPs."""
+    cfg = cmpc.reference_config("par", ctype, p=20)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", ctype))
+    lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
+    with cmpc.Context(cfg, B) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u, du, ws)
+        ctx.upload_lin(lin)
+        ctx.build()
+        ctx.init_warmstart()
+        ctx.iterate(1)
+        assert ctx.last_solve_kernel() == solve
+        ctx.step(2)
+        assert ctx.last_step_fused() == fused
 
 
 FUSED_CASES = [  # plant, controller, p, K, B scenarios (the kernel AUTO fuses on)
@@ -120,12 +128,16 @@ FUSED_CASES = [  # plant, controller, p, K, B scenarios (the kernel AUTO fuses o
 ]
 
 
-def _run_step(cfg, arr, lin, u, du, ws, K, variant, steps=3):
+def _run_step(cfg, arr, lin, u, du, ws, K, variant, build=None, steps=3):
+    """three steps; returns the per-step results and the build kernel used
+    (a split run pins `build`: the two build kernels differ in rounding)"""
     out = []
     with cmpc.Context(cfg, lin.shape[0] // cfg.S) as ctx:
         ctx.configure(arr)
         ctx.set_state(u, du, ws)
         ctx.upload_lin(lin)
+        if build is not None:
+            ctx.set_build_variant(build)
         ctx.build()
         ctx.init_warmstart()
         ctx.set_step_variant(variant)
@@ -134,10 +146,11 @@ def _run_step(cfg, arr, lin, u, du, ws, K, variant, steps=3):
         for step in range(steps):
             ctx.step(K, cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE)
             assert ctx.last_step_fused() == (variant == cmpc.CMPC_STEP_FUSED)
+            kind = ctx.last_build_kernel()
             d, st, nw = ctx.download()
             tr, ntr = ctx.download_trace(K)
             out.append((d, st, nw, *ctx.get_state(), tr, ntr, *ctx.download_qp()))
-    return out
+    return out, kind
 
 
 @pytest.mark.parametrize("plant,ctype,p,K,B", FUSED_CASES)
@@ -148,8 +161,8 @@ def test_gpu_fused_step_equals_split_step(plant, ctype, p, K, B):
     cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = _tight(cmpc.controller_arrays(cfg, reference_setup(plant, ctype)), 0.5)
     lin, u, du, ws = synthetic_batch(cfg, B, seed=70 + p, n_distinct=min(B, 512))
-    split = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_SPLIT)
-    fused = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_FUSED)
+    fused, kind = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_FUSED)
+    split, _ = _run_step(cfg, arr, lin, u, du, ws, K, cmpc.CMPC_STEP_SPLIT, build=kind)
     names = ("du", "status", "nwsr", "u_old", "du_old", "ws", "trace", "ntrace", "H", "f", "G")
     for step, (a, b) in enumerate(zip(split, fused)):
         for name, x, y in zip(names, a, b):

@@ -69,17 +69,18 @@ def main():
     bk = "cmpc_build_rows_kernel" if "cmpc_build_rows_kernel" in summary["kernels"] else "cmpc_build_kernel"
     b = summary["kernels"].get(bk, {})
     if "hbm_bytes_per_launch" in b:
-        # the hash of the sources the PMC pass ran on, as that run's bench line
-        # printed it (the tree here may have moved on since)
+        # the hash of the bench kernel's machine code the PMC pass ran, as that
+        # run's bench line printed it (the tree here may have moved on since)
         h = None
         try:
             h = json.load(open(os.path.join(OUT, f"pmc{tag}_fetch.json")))["roofline"]["traffic_provenance"][
-                "current_source_hash"]
+                "current_code_hash"]
         except (OSError, ValueError, KeyError, TypeError):
             sys.path.insert(0, ROOT)
-            from bench import build_source_hash
-            h = build_source_hash()
-        json.dump({"batch": batch, "round": rnd, "kernel": bk, "build_source_hash": h,
+            sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
+            from bench import bench_kernel_code_hash
+            h = bench_kernel_code_hash()
+        json.dump({"batch": batch, "round": rnd, "kernel": bk, "build_kernel_code_hash": h,
                    "hbm_bytes_per_launch": b["hbm_bytes_per_launch"],
                    "hbm_read_bytes": b["hbm_read_bytes"], "hbm_write_bytes": b["hbm_write_bytes"],
                    "source": f"profiles/{rnd}_pmc.json"},
