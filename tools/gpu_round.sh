@@ -4,11 +4,11 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-r2}
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/test_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
+timeout -k 10 900 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --headline-only > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
 pmc() {  # name, counters...   (separate passes, kernel trace only)

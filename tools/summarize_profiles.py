@@ -7,7 +7,8 @@ usage: python tools/summarize_profiles.py TAG ROUND [BATCH]
   gpurun_out/pmcTAG_{sq1,sq2,fetch,write}/...   -> profiles/ROUND_pmc.json
                                                  + profiles/pmc_build_coop_p50.json
 
-HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+Counters are the median over a kernel's dispatches.  HBM bytes per launch
+follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
 bytes of a 16-byte-per-lane coalesced streaming read (the build kernel's record
 loads are exactly that), so it is doubled; WRITE_SIZE is taken as is.
@@ -31,7 +32,14 @@ def counters(tag, name):
     acc = defaultdict(lambda: defaultdict(list))
     for row in csv.DictReader(open(path)):
         acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} | {"_dispatches": len(next(iter(d.values())))}
+    # the median over a kernel's dispatches: a launch right after one that
+    # left many dirty L2 lines (e.g. a traced solve) is charged their
+    # write-back, which the mean would spread over the others
+    def med(v):
+        v = sorted(v)
+        n = len(v)
+        return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+    return {k: {c: med(v) for c, v in d.items()} | {"_dispatches": len(next(iter(d.values())))}
             for k, d in acc.items()}
 
 
