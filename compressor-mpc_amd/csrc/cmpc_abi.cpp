@@ -1710,7 +1710,7 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   // solve: B = 1 28.2 vs 33.1 us fused on the row kernel)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
   const bool rows_fill_ = (c->nqp + 3) / 4 >= 4 * (c->cus > 0 ? c->cus : 256);
-  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && (c->d.S == 1 || rows_fill_);
+  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && (c->d.S == 1 ? !rows_fill_ : rows_fill_);
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
                     (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);

@@ -1,0 +1,149 @@
+// K Jacobi iterations of one QP per lane (qp_solver.h): the body of the
+// iterate kernel (cmpc_solve_kernel) and of the fused small-batch step of the
+// row build kernel (build_rows.hip), which solves the four QPs it just built
+// in lanes 0-3 of the same wave.
+//
+// rec = the QP's H, f (nV*nV, nV; global or LDS), G[a][c] = gb[(a * NVOA + c)
+// * gstride]; q the QP (clamped), active = stores allowed; s = its
+// sub-controller, base_lane = the lane of the scenario's sub-controller 0
+// (the plan exchange reads lanes base_lane + s2 of the same wave).
+#pragma once
+#include "cmpc_internal.h"
+#include "qp_solver.h"
+
+#ifndef CMPC_SOLVE_CACHE
+#define CMPC_SOLVE_CACHE 1  // reuse the working-set factors across Jacobi iterations
+#endif
+#ifndef CMPC_SOLVE_PRIO
+#define CMPC_SOLVE_PRIO 1  // priority by Jacobi-iteration progress (iterate 0.049 -> 0.047 ms)
+#endif
+
+template <int N, int NU, int NVO, bool TRACE, bool EXT>
+__device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool active, int s, int base_lane,
+                                              const double* rec, const double* gb, int gstride) {
+  constexpr int M = N / NU;
+  constexpr int NVOA = NVO > 0 ? NVO : 1;
+  constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
+  const double* cfg = P.cfg + (size_t)s * P.co.len;
+  double H[N][N], f[N];
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+#pragma unroll
+    for (int b = 0; b < N; ++b) H[a][b] = rec[a * N + b];
+#pragma unroll
+  for (int a = 0; a < N; ++a) f[a] = rec[N * N + a];
+
+  // bounds repeat every NU entries (rep_m(lower - u_old), rep_m(rate bounds));
+  // H^-1 stays in registers (an LDS copy measured slower: the compiler
+  // hoists its loads and spills more)
+  Qp<N, NU, NU> qp;
+  double uo[NU];
+#pragma unroll
+  for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
+#pragma unroll
+  for (int c = 0; c < NU; ++c) {
+    qp.lb[c] = cfg[P.co.lower + c] - uo[c];
+    qp.ub[c] = cfg[P.co.upper + c] - uo[c];
+    qp.lbA[c] = cfg[P.co.rlower + c];
+    qp.ubA[c] = cfg[P.co.rupper + c];
+  }
+  qp.tolerances();
+  const bool pd = hinv_of<N>(H, qp.Hinv);
+  double hmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) hmax = fabs(H[i][i]) > hmax ? fabs(H[i][i]) : hmax;
+  const double tol_d = TOL_D * (1.0 + hmax);
+
+  uint32_t ws = P.ws[q];
+  double x[N];
+  QpOut o;
+  if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
+    qp_solve_t<false>(qp, pd, tol_d, f, 0u, CMPC_NWSR_MAX, x, o);
+    if (active) P.ws[q] = o.ws;
+    return;
+  }
+  double dprev[N];
+#pragma unroll
+  for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+#if CMPC_SOLVE_CACHE
+  // working set + factors of the previous Jacobi iteration's solve (same H):
+  // reused when the working set is unchanged (qp_solve_t, CACHE)
+  WSet<N> wc;
+  uint32_t wc_ws = kWsInvalid;
+#endif
+  for (int k = 0; k < P.K; ++k) {
+#if CMPC_SOLVE_PRIO
+    {  // fair progress of the SIMD's waves (cf. build_rows.hip)
+      const int level = 3 - (4 * k) / (P.K > 0 ? P.K : 1);
+      if (level <= 0) __builtin_amdgcn_s_setprio(0);
+      else if (level == 1) __builtin_amdgcn_s_setprio(1);
+      else if (level == 2) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+    }
+#endif
+    double fk[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) fk[a] = f[a];
+    if (NVO > 0 && CMPC_QP_ABL != 3) {
+      double dother[NVOA];
+      if constexpr (EXT) {
+        // du_last of DistributedController::GetInput: the other controllers'
+        // plans, controller-major, then move, then input (nerve_center.h:283-285)
+#pragma unroll
+        for (int rk = 0; rk < SM1; ++rk)
+#pragma unroll
+          for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = P.du_other[(size_t)q * NVO + rk * N + mv * NU + c];
+      } else {
+#pragma unroll
+        for (int rk = 0; rk < SM1; ++rk) {
+          const int s2 = rk + (rk >= s ? 1 : 0);
+#pragma unroll
+          for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+            for (int c = 0; c < NU; ++c)
+              dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + s2, 64);
+        }
+      }
+      // f_k = f + (Su_other du_other)' W Su  ==  f + G du_other
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        double t = fk[a];
+#pragma unroll
+        for (int c = 0; c < NVOA; ++c) t = t + gb[(a * NVOA + c) * gstride] * dother[c];
+        fk[a] = t;
+      }
+    }
+#if CMPC_SOLVE_CACHE
+    qp_solve_t<TRACE, true>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o, &wc, &wc_ws);
+#else
+    qp_solve_t<TRACE>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
+#endif
+    ws = o.ws;
+#pragma unroll
+    for (int a = 0; a < N; ++a) dprev[a] = x[a];
+    if (TRACE && active && P.trace) {
+      uint32_t* tr = reinterpret_cast<uint32_t*>(P.trace + ((size_t)q * P.K + k) * 16);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) tr[t] = o.tr[t];
+      P.ntrace[(size_t)q * P.K + k] = o.ntrace;
+    }
+  }
+  if (!active) return;
+  P.ws[q] = ws;
+  if (P.K > 0) {
+    P.status[q] = o.status;
+    P.nwsr[q] = o.nchg;
+  }
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    P.du[(size_t)q * N + a] = dprev[a];
+    P.du_old[(size_t)q * N + a] = dprev[a];
+  }
+  if (P.flags & CMPC_APPLY_MOVE) {
+#pragma unroll
+    for (int c = 0; c < NU; ++c) P.u_old[(size_t)q * P.nu_tot + c] = uo[c] + dprev[c];
+  }
+}

@@ -1,0 +1,21 @@
+#!/bin/bash
+# small-batch round: parity of the fused/row kernels, then timings and diagnostics
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+TAG=${1:-r4c}
+timeout -k 10 900 python -u -m pytest tests/test_gpu_small_batch.py tests/test_multirank.py tests/test_cpp_adapter.py -m gpu -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/test_$TAG.log
+[ $rc -ne 0 ] && exit $rc
+OUT=gpurun_out/small_$TAG.txt
+timeout -k 10 300 python -u tools/time_small.py c5 c2 b1 c1b1 > $OUT 2>&1 || exit $?
+echo "== rows timing p=20 B=4096" >> $OUT
+CMPC_LIBRARY=ab/timing/libcmpc.so timeout -k 10 120 python -u tools/rows_timing.py 20 4096 >> $OUT 2>&1 || exit $?
+echo "== rows timing p=50 B=1" >> $OUT
+CMPC_LIBRARY=ab/timing/libcmpc.so timeout -k 10 120 python -u tools/rows_timing.py 50 1 >> $OUT 2>&1 || exit $?
+echo "== build vs p, B=4096" >> $OUT
+CMPC_TB_VARIANT=both timeout -k 10 200 python -u tools/time_build.py 4096 2 10 20 50 >> $OUT 2>&1 || exit $?
+echo "== build vs p, B=1" >> $OUT
+CMPC_TB_VARIANT=both timeout -k 10 200 python -u tools/time_build.py 1 2 10 20 50 >> $OUT 2>&1 || exit $?
+echo "== microbench chain" >> $OUT
+timeout -k 10 120 tools/microbench_chain >> $OUT 2>&1 || exit $?
+echo ALLDONE >> $OUT

@@ -87,7 +87,7 @@ int main() {
   long long* cyc;
   hipMalloc(&out, sizeof(double) * 256 * 256 * 8);
   hipMalloc(&cyc, sizeof(long long));
-  for (int bpc : {2, 3, 4, 6, 8}) {
+  for (int bpc : {1, 2, 3, 4, 8}) {
     run<0>("A 13 indep acc, fixed operands", out, cyc, bpc);
     run<1>("B dependent chain, 13 distinct m (prop)", out, cyc, bpc);
     run<2>("C 13 indep acc, distinct m", out, cyc, bpc);

@@ -1,6 +1,6 @@
 """Per-phase cycle attribution of the row build kernel (diagnostic library
 built with -DCMPC_ROWS_TIMING=1: tools/ablate/libcmpc_timing.so).
-usage: CMPC_LIBRARY=.../libcmpc_timing.so python tools/rows_timing.py [p]"""
+usage: CMPC_LIBRARY=.../libcmpc_timing.so python tools/rows_timing.py [p] [B] [plant-ctype]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
@@ -9,10 +9,11 @@ import cmpc
 from cmpc.configs import reference_setup
 from cmpc.synthetic import synthetic_batch
 p = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-B = 65536
-cfg = cmpc.reference_config("par", "coop", p=p)
-arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
-lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=256)
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+PLANT, CTYPE = (sys.argv[3] if len(sys.argv) > 3 else "par-coop").split("-")
+cfg = cmpc.reference_config(PLANT, CTYPE, p=p)
+arr = cmpc.controller_arrays(cfg, reference_setup(PLANT, CTYPE))
+lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=min(B, 256))
 with cmpc.Context(cfg, B) as ctx:
     ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
     ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
@@ -22,8 +23,11 @@ with cmpc.Context(cfg, B) as ctx:
         for _ in range(16):
             ctx.build()
         ctx.synchronize()
+    ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
     ctx.build()
     ctx.synchronize()
+    kms, _ = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+    print(f"build kernel (events): {kms * 1e3:.2f} us")
     H, f, G = ctx.download_qp()
 raw = np.concatenate([H.reshape(H.shape[0], -1), f, G.reshape(G.shape[0], -1)], axis=1).reshape(-1)
 d = raw[: (raw.size // 16) * 16].reshape(-1, 16)
