@@ -129,7 +129,11 @@ void cmpc_build_rows_kernel(BuildParams P) {
   // software-pipelined LDS consumption (CMPC_ROWS_SPLIT, CMPC_ROWS_AS0; round
   // 3) where the registers allow it without scratch: the parallel plant's
   // coop / ncoop kernels with plain lines (the bench kernel among them)
-  constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 && NY <= 3 && NV <= 4 && !RING;
+  // (round 4: also every instantiation compiled for two or fewer waves per
+  // SIMD -- the 256-register ring, ny = 4 and nV = 8 kernels of long
+  // horizons: bit-identical, ser-coop p = 100 -1.2 %, par-cent p = 200
+  // -0.5 %, profiles/r3_pipe_wpe2_ab.txt)
+  constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 && ((NY <= 3 && NV <= 4 && !RING) || WPE <= 2);
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

@@ -34,81 +34,86 @@ def settle(ctx, K, sec=0.3):
         ctx.synchronize()
 
 
-for name in (sys.argv[1:] or ["c5", "c2", "b1"]):
-    plant, ctype, p, B, K = CONFIGS[name]
-    cfg = cmpc.reference_config(plant, ctype, p=p)
-    arr = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
-    lin, u, du, ws = synthetic_batch(cfg, B, seed=11, n_distinct=min(B, 2048))
-    with cmpc.Context(cfg, B) as ctx:
-        ctx.configure(arr)
-        ctx.set_state(u, du, ws)
-        ctx.upload_lin(lin)
-        ctx.build()
-        ctx.init_warmstart()
-        settle(ctx, K)
-        res = []
-        for vn, v in VARS:
-            try:
-                ctx.set_build_variant(v)
-                ctx.build()
-            except Exception as e:  # noqa: BLE001
-                res.append(f"{vn} n/a")
-                continue
-            ctx.synchronize()
-            ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
-            for _ in range(REPS):
-                ctx.build()
-            ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
-            ctx.enable_timing(False)
-            res.append(f"{vn} {ms / n * 1e3:7.2f}")
-        ctx.set_build_variant(cmpc.CMPC_BUILD_AUTO)
-        its = []
-        for sv, sn in ((getattr(cmpc, "CMPC_SOLVE_LANE", None), "lane"), (getattr(cmpc, "CMPC_SOLVE_ROWS", None), "rows")):
-            if sv is None:
-                continue
-            ctx.set_solve_variant(sv)
-            for k in (0, 1, K):
-                ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
-                for _ in range(REPS):
-                    ctx.iterate(k)
-                ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
-                ctx.enable_timing(False)
-                its.append(f"{sn} K={k} {ms / n * 1e3:6.2f}")
-        if hasattr(cmpc, "CMPC_SOLVE_AUTO"):
-            ctx.set_solve_variant(cmpc.CMPC_SOLVE_AUTO)
-        steps = []
-        variants = [("split", getattr(cmpc, "CMPC_STEP_SPLIT", None)), ("fused", getattr(cmpc, "CMPC_STEP_FUSED", None)),
-                    ("auto", getattr(cmpc, "CMPC_STEP_AUTO", None))]
-        for vn, v in variants:
-            if v is None and vn != "auto":
-                continue
-            try:
-                if v is not None:
-                    ctx.set_step_variant(v)
-                ctx.step(K)
-                ctx.synchronize()
-            except Exception:  # noqa: BLE001
-                steps.append(f"{vn} n/a")
-                continue
-            settle(ctx, K, 0.1)
-            t0 = time.perf_counter()
-            for _ in range(REPS):
-                ctx.step(K)
-            ctx.synchronize()
-            t_bb = (time.perf_counter() - t0) / REPS
-            t0 = time.perf_counter()
-            for _ in range(REPS):
-                ctx.step(K)
-                ctx.synchronize()
-            t_sync = (time.perf_counter() - t0) / REPS
-            kern = ""
-            if vn == "fused":
-                ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_STEP,))
-                for _ in range(REPS):
-                    ctx.step(K)
-                ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_STEP)
-                ctx.enable_timing(False)
-                kern = f" kernel {ms / n * 1e3:.2f}"
-            steps.append(f"{vn} {t_bb * 1e6:.1f}/{t_sync * 1e6:.1f}{kern}")
-    print(f"{name:5s} {plant}-{ctype} p={p} B={B} K={K}  build us: {', '.join(res)} | iterate us: "
-          f"{', '.join(its)} | step us back-to-back/synchronised: {'; '.join(steps)}", flush=True)
+def main():
+  for name in (sys.argv[1:] or ["c5", "c2", "b1"]):
+      plant, ctype, p, B, K = CONFIGS[name]
+      cfg = cmpc.reference_config(plant, ctype, p=p)
+      arr = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
+      lin, u, du, ws = synthetic_batch(cfg, B, seed=11, n_distinct=min(B, 2048))
+      with cmpc.Context(cfg, B) as ctx:
+          ctx.configure(arr)
+          ctx.set_state(u, du, ws)
+          ctx.upload_lin(lin)
+          ctx.build()
+          ctx.init_warmstart()
+          settle(ctx, K)
+          res = []
+          for vn, v in VARS:
+              try:
+                  ctx.set_build_variant(v)
+                  ctx.build()
+              except Exception as e:  # noqa: BLE001
+                  res.append(f"{vn} n/a")
+                  continue
+              ctx.synchronize()
+              ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+              for _ in range(REPS):
+                  ctx.build()
+              ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+              ctx.enable_timing(False)
+              res.append(f"{vn} {ms / n * 1e3:7.2f}")
+          ctx.set_build_variant(cmpc.CMPC_BUILD_AUTO)
+          its = []
+          for sv, sn in ((getattr(cmpc, "CMPC_SOLVE_LANE", None), "lane"), (getattr(cmpc, "CMPC_SOLVE_ROWS", None), "rows")):
+              if sv is None:
+                  continue
+              ctx.set_solve_variant(sv)
+              for k in (0, 1, K):
+                  ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
+                  for _ in range(REPS):
+                      ctx.iterate(k)
+                  ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
+                  ctx.enable_timing(False)
+                  its.append(f"{sn} K={k} {ms / n * 1e3:6.2f}")
+          if hasattr(cmpc, "CMPC_SOLVE_AUTO"):
+              ctx.set_solve_variant(cmpc.CMPC_SOLVE_AUTO)
+          steps = []
+          variants = [("split", getattr(cmpc, "CMPC_STEP_SPLIT", None)), ("fused", getattr(cmpc, "CMPC_STEP_FUSED", None)),
+                      ("auto", getattr(cmpc, "CMPC_STEP_AUTO", None))]
+          for vn, v in variants:
+              if v is None and vn != "auto":
+                  continue
+              try:
+                  if v is not None:
+                      ctx.set_step_variant(v)
+                  ctx.step(K)
+                  ctx.synchronize()
+              except Exception:  # noqa: BLE001
+                  steps.append(f"{vn} n/a")
+                  continue
+              settle(ctx, K, 0.1)
+              t0 = time.perf_counter()
+              for _ in range(REPS):
+                  ctx.step(K)
+              ctx.synchronize()
+              t_bb = (time.perf_counter() - t0) / REPS
+              t0 = time.perf_counter()
+              for _ in range(REPS):
+                  ctx.step(K)
+                  ctx.synchronize()
+              t_sync = (time.perf_counter() - t0) / REPS
+              kern = ""
+              if vn == "fused":
+                  ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_STEP,))
+                  for _ in range(REPS):
+                      ctx.step(K)
+                  ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_STEP)
+                  ctx.enable_timing(False)
+                  kern = f" kernel {ms / n * 1e3:.2f}"
+              steps.append(f"{vn} {t_bb * 1e6:.1f}/{t_sync * 1e6:.1f}{kern}")
+      print(f"{name:5s} {plant}-{ctype} p={p} B={B} K={K}  build us: {', '.join(res)} | iterate us: "
+            f"{', '.join(its)} | step us back-to-back/synchronised: {'; '.join(steps)}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
