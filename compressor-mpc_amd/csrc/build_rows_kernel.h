@@ -652,9 +652,13 @@ void cmpc_build_rows_kernel(BuildParams P) {
     // iterate kernel's solver, lane_solve.h) once the build's registers are
     // dead: lane 4 i + r takes QP r of the wave's i-th group; a scenario's
     // sub-controllers share a quad (S divides 4), their plans exchanged by
-    // lane shuffles.  The agent-scope fence makes the wave's own QP stores
-    // visible to its loads.
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    // lane shuffles.  The wave reads back its own QP stores once they have
+    // completed (vmcnt(0)): the vector L0 is invalidated at kernel start and
+    // is write-through, and no lane of the kernel reads a QP before its
+    // group's wave has stored it, so the loads see the stores.  (An
+    // agent-scope fence instead writes back the whole L2: 85 us a step at
+    // SURVEY config 2, tools/time_small.py.)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     constexpr int NVO = M * (NUT - NU);
     const int gi = g_first + (lane >> 2) * nwaves;
     if (gi < ngroups) {
@@ -663,7 +667,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
       const int qc = al ? ql : nqp - 1;
       const int sl = qc & (S - 1);
       const double* qr = P.qp + (size_t)qc * P.qp_len;
-      lane_solve_qp<NV, NU, NVO, FUSE == 4, false>(P.sv, qc, al, sl, lane - sl, qr, qr + NV * NV + NV, 1);
+      lane_solve_qp<NV, NU, NVO, FUSE == 4, false, 1>(P.sv, qc, al, sl, lane - sl, qr, qr + NV * NV + NV);
     }
   }
 #if CMPC_ROWS_TIMING

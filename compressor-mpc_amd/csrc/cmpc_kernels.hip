@@ -606,8 +606,8 @@ void cmpc_solve_kernel(SolveParams P) {
     for (int c = 0; c < NVOA; ++c)
       gsh[a * NVOA + c][threadIdx.x] = (NVO > 0) ? rec[N * N + N + a * NVO + c] : 0.0;
 
-  lane_solve_qp<N, NU, NVO, TRACE, EXT>(P, q, active, s, base_lane, rec, &gsh[0][threadIdx.x],
-                                        CMPC_SOLVE_THREADS);
+  lane_solve_qp<N, NU, NVO, TRACE, EXT, CMPC_SOLVE_THREADS>(P, q, active, s, base_lane, rec,
+                                                           &gsh[0][threadIdx.x]);
 }
 
 // standalone batched solve (parity and KKT tests)

@@ -3,8 +3,8 @@
 // row build kernel (build_rows.hip), which solves the four QPs it just built
 // in lanes 0-3 of the same wave.
 //
-// rec = the QP's H, f (nV*nV, nV; global or LDS), G[a][c] = gb[(a * NVOA + c)
-// * gstride]; q the QP (clamped), active = stores allowed; s = its
+// rec = the QP's H, f (nV*nV, nV; global, LDS or registers), G[a][c] =
+// gb[(a * NVOA + c) * GSTRIDE]; q the QP (clamped), active = stores allowed; s = its
 // sub-controller, base_lane = the lane of the scenario's sub-controller 0
 // (the plan exchange reads lanes base_lane + s2 of the same wave).
 #pragma once
@@ -18,9 +18,9 @@
 #define CMPC_SOLVE_PRIO 1  // priority by Jacobi-iteration progress (iterate 0.049 -> 0.047 ms)
 #endif
 
-template <int N, int NU, int NVO, bool TRACE, bool EXT>
+template <int N, int NU, int NVO, bool TRACE, bool EXT, int GSTRIDE>
 __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool active, int s, int base_lane,
-                                              const double* rec, const double* gb, int gstride) {
+                                              const double* rec, const double* gb) {
   constexpr int M = N / NU;
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
@@ -112,7 +112,7 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
       for (int a = 0; a < N; ++a) {
         double t = fk[a];
 #pragma unroll
-        for (int c = 0; c < NVOA; ++c) t = t + gb[(a * NVOA + c) * gstride] * dother[c];
+        for (int c = 0; c < NVOA; ++c) t = t + gb[(a * NVOA + c) * GSTRIDE] * dother[c];
         fk[a] = t;
       }
     }

@@ -115,3 +115,13 @@ def test_gpu_sim_host_entry_points_match_device_ones(plant, B):
         for p, q in zip(a, b):
             assert np.array_equal(p, q)
         assert not a[3].any()
+
+
+def test_setup_file_text_roundtrip():
+    """SetupFile.text() (the writer bench.py uses for the C++ latency harness)
+    parses back to the same SetupFile for every reference setup."""
+    from cmpc.configs import SetupFile, reference_config, reference_setup
+    for plant in ("par", "ser"):
+        for ctype in ("cent", "coop", "ncoop"):
+            st = reference_setup(plant, ctype)
+            assert SetupFile.parse(st.text(), reference_config(plant, ctype)) == st
