@@ -71,13 +71,18 @@
 #if CMPC_EXP == 5
 #define CMPC_EXP_STEP(pv, m, a, va, acc)                  \
   {                                                       \
+    va = __builtin_fma(smask, va, rd);                    \
     double a1_ = 0.0;                                     \
     prop2w_dpp<NS, ND>(pv, m, a, a1_);                    \
     a = a + a1_;                                          \
     CMPC_EXP_GACC(va, acc);                               \
   }
 #elif CMPC_EXP == 6
-#define CMPC_EXP_STEP(pv, m, a, va, acc) prop1w_gacc_dpp<NS, ND, NUT, NU, M>(pv, m, a, va, acc)
+#define CMPC_EXP_STEP(pv, m, a, va, acc)                  \
+  {                                                       \
+    va = __builtin_fma(smask, va, rd);                    \
+    prop1w_gacc_dpp<NS, ND, NUT, NU, M>(pv, m, a, va, acc); \
+  }
 #elif CMPC_BUILD_ILP > 1
 // several partial accumulators per chain (small batches: one wave per SIMD
 // has no other wave to hide the dependent FP64 latency); the gather column
@@ -93,11 +98,31 @@
     CMPC_EXP_GACC(va, acc);                                                \
   }
 #else
-#define CMPC_EXP_STEP(pv, m, a, va, acc) \
-  {                                      \
-    CMPC_EXP_PROP(pv, m, a);             \
-    CMPC_EXP_GACC(va, acc);              \
+// the gather column update consumes the previous step's hand-off read (rd)
+// after the chain, so the LDS round trip hides behind it
+#define CMPC_EXP_STEP(pv, m, a, va, acc)  \
+  {                                       \
+    CMPC_EXP_PROP(pv, m, a);              \
+    va = __builtin_fma(smask, va, rd);    \
+    CMPC_EXP_GACC(va, acc);               \
   }
+#endif
+
+// Diagnostic build (tools/rows_timing.py ... wave): per-wave s_memtime cycle
+// totals of the QP phases of the one-QP-per-wave kernel, written over the QP
+// output as the row kernel's CMPC_ROWS_TIMING (results invalid).
+#ifndef CMPC_WAVE_TIMING
+#define CMPC_WAVE_TIMING 0
+#endif
+#if CMPC_WAVE_TIMING
+#define CMPC_WT(i)                                         \
+  {                                                        \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();    \
+    tsum[i] += now_ - tlast;                               \
+    tlast = now_;                                          \
+  }
+#else
+#define CMPC_WT(i)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -273,7 +298,12 @@ void cmpc_build_kernel(BuildParams P) {
   const int share = (P.nqp + nwaves - 1) / nwaves;
   int done_qp = 0;
   __builtin_amdgcn_s_setprio(3);
+#if CMPC_WAVE_TIMING
+  uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  const uint64_t t0c = tlast, t0r = __builtin_amdgcn_s_memrealtime();
+#endif
   for (; q < P.nqp; q += nwaves) {
+    CMPC_WT(5)  // back-edge
     {
       const int level = 3 - (4 * done_qp) / share;
       if (level <= 0) __builtin_amdgcn_s_setprio(0);
@@ -302,6 +332,7 @@ void cmpc_build_kernel(BuildParams P) {
       }
       uold_l = (qn < P.nqp && lane < NUT) ? P.u_old[(size_t)qn * NUT + lane] : 0.0;
     }
+    CMPC_WT(0)  // staging
     const double* Cs = recl + P.off_C;
     const double* xa = recl + P.off_x;
     // C_hat = L_W' C_sel (ny x nobs), one element per lane
@@ -356,15 +387,20 @@ void cmpc_build_kernel(BuildParams P) {
       double spv = *(s_st ? recl + P.off_f + col : s_w ? wl + NY + skw : zero_p);
 #pragma unroll
       for (int k = 0; k < ND; ++k) spv += sm[NS + k] * wl[k];  // x_1 = f + Adelay w_0
-      double syh = s_w ? wl[2 * NY + skw] : yl[soz];
+      // chain init of step r formed at the end of step r - 1 from an operand
+      // read one step earlier still (the LDS latency hides behind a chain;
+      // the last step reads one entry past the table, inside the block)
+      double san = __builtin_fma(-sym, s_w ? wl[2 * NY + skw] : yl[soz], sbase);
       const double* sylp = s_w ? wl + 3 * NY + skw : yl + NY + soz;
+      double syh = sylp[0];
       const bool zlane = row == 3 && s_out;
       double* zq = zl + soz * P.zl_stride;
 #define CMPC_PRE_STEP(u)                          \
   {                                               \
-    double a = __builtin_fma(-sym, syh, sbase);   \
+    double a = san;                               \
     prop1w_dpp<NS, ND>(spv, sm, a);               \
-    syh = sylp[(u) * NY];                         \
+    san = __builtin_fma(-sym, syh, sbase);        \
+    syh = sylp[((u) + 1) * NY];                   \
     spv = a;                                      \
     if (zlane) zq[u] = a;                         \
   }
@@ -406,9 +442,14 @@ void cmpc_build_kernel(BuildParams P) {
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
     double va = 0.0;  // gather lane: QP column value of the previous row
     double rd = 0.0;  // gather lane: raw value read at the end of the previous step
-    // per-step operand: yhat_r (output lanes) / w_{r+2} (carrier lanes)
+    // per-step operand: yhat_r (output lanes) / w_{r+2} (carrier lanes); the
+    // chain init `an` of step r + 1 is formed at the end of step r from the
+    // operand read during step r - 1 (two steps of LDS read-ahead; the last
+    // step reads one entry past the table, inside the LDS block)
     double yh = wlane ? wl[2 * NY + kw] : yl[oz];
     const double* ylp = wlane ? wl + 3 * NY + kw : yl + NY + oz;
+    double an = __builtin_fma(-ym, yh, base);
+    if constexpr (!PRE) yh = ylp[0];
     double* wq = wp;
     const double* rq = rp;
 
@@ -416,16 +457,17 @@ void cmpc_build_kernel(BuildParams P) {
 #define CMPC_BUILD_STEP(u)                                                             \
   {                                                                                    \
     /* chain init: f (states), kappa - yhat_r (outputs), w_{r+2} (carriers) */         \
-    double a = __builtin_fma(-ym, yh, base);                                           \
-    /* accumulate row r-1: acc[a] += column_a * own column (gather lanes) */          \
-    if constexpr (CMPC_BUILD_ILP == 1) va = __builtin_fma(smask, va, rd);              \
+    double a = an;                                                                     \
+    /* chain; accumulate row r-1: acc[a] += column_a * own column (gather lanes) */   \
     CMPC_EXP_STEP(pv, m, a, va, acc);                                                  \
-    CMPC_EXP_YH(if constexpr (!PRE) yh = ylp[(u) * NY]);                               \
+    if constexpr (!PRE) an = __builtin_fma(-ym, yh, base);                             \
+    CMPC_EXP_YH(if constexpr (!PRE) yh = ylp[((u) + 1) * NY]);                         \
     /* a: P rows -> P_{r+1} / raw Markov of step r; sim lanes -> x_{r+2} / z_r */      \
     pv = a;                                                                            \
     CMPC_EXP_HAND(if (mlane || slane) wq[u] = a; rd = rq[u];)                          \
   }
 
+    CMPC_WT(2)  // prologue compute
     int r = 0;
     int rinc_q = rinc;
     for (int seg = 0; seg <= nbound; ++seg) {
@@ -457,6 +499,7 @@ void cmpc_build_kernel(BuildParams P) {
     va = __builtin_fma(smask, va, rd);
     gacc_dpp<NUT, NU, M>(va, acc);  // row p-1
     // (the accumulation at r = 0 adds products of the zero initial va)
+    CMPC_WT(3)  // horizon loop
 
     // reduce over the ny rows through LDS; row 0 of the gather lanes stores
     if (red_lane) {
@@ -519,9 +562,11 @@ void cmpc_build_kernel(BuildParams P) {
       const double f_l = (col < N) ? sel<N>(Fv, col) : 0.0;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // the totals are read before the scratch is written
+      CMPC_WT(4)  // epilogue
       rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
                                                 red + NY * NG * NV + row * N * N);
       __builtin_amdgcn_wave_barrier();
+      CMPC_WT(1)  // fused solve
       continue;
     }
     if (row == 0 && col < NG) {
@@ -553,7 +598,26 @@ void cmpc_build_kernel(BuildParams P) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    CMPC_WT(4)  // epilogue
   }
+#if CMPC_WAVE_TIMING
+  // slots as CMPC_ROWS_TIMING: 0 staging, 1 fused solve, 2 prologue, 3 loop,
+  // 4 epilogue, 5 back-edge; 6 QPs, 7 marker, 8-11 clocks, 12-14 placement
+  if (lane == 0) {
+    const uint64_t t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
+    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 16;
+    for (int i = 0; i < 6; ++i) dbg[i] = (double)tsum[i];
+    dbg[6] = done_qp;
+    dbg[7] = 1.0;
+    dbg[8] = (double)(t1c - t0c);
+    dbg[9] = (double)(t1r - t0r);
+    dbg[10] = (double)t0r;
+    dbg[11] = (double)t1r;
+    dbg[12] = (double)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    dbg[13] = (double)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    dbg[14] = (double)(blockIdx.x * CMPC_BUILD_WAVES + wave);
+  }
+#endif
 }
 
 #include "lane_solve.h"

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-r4c}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_small_batch.py tests/test_multirank.py tests/test_cpp_adapter.py -m gpu -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/test_$TAG.log
 [ $rc -ne 0 ] && exit $rc
 OUT=gpurun_out/small_$TAG.txt

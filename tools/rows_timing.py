@@ -1,6 +1,8 @@
-"""Per-phase cycle attribution of the row build kernel (diagnostic library
-built with -DCMPC_ROWS_TIMING=1: tools/ablate/libcmpc_timing.so).
-usage: CMPC_LIBRARY=.../libcmpc_timing.so python tools/rows_timing.py [p] [B] [plant-ctype]"""
+"""Per-phase cycle attribution of the row build kernel, or with KERNEL=wave of
+the one-QP-per-wave kernel (diagnostic library built with -DCMPC_ROWS_TIMING=1
+-DCMPC_WAVE_TIMING=1: tools/build_variant.sh timing "...").  For the wave
+kernel slot 1 is the fused solve (0 here) and a "group" is one QP.
+usage: CMPC_LIBRARY=ab/timing/libcmpc.so python tools/rows_timing.py [p] [B] [plant-ctype] [rows|wave]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "compressor-mpc_amd"))
@@ -11,12 +13,13 @@ from cmpc.synthetic import synthetic_batch
 p = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 PLANT, CTYPE = (sys.argv[3] if len(sys.argv) > 3 else "par-coop").split("-")
+KERNEL = sys.argv[4] if len(sys.argv) > 4 else "rows"
 cfg = cmpc.reference_config(PLANT, CTYPE, p=p)
 arr = cmpc.controller_arrays(cfg, reference_setup(PLANT, CTYPE))
 lin, u, du, ws = synthetic_batch(cfg, B, seed=7, n_distinct=min(B, 256))
 with cmpc.Context(cfg, B) as ctx:
     ctx.configure(arr); ctx.set_state(u, du, ws); ctx.upload_lin(lin)
-    ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
+    ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS if KERNEL == "rows" else cmpc.CMPC_BUILD_WAVE)
     import time
     t_end = time.perf_counter() + 0.3  # settle at the steady clock
     while time.perf_counter() < t_end:
@@ -36,7 +39,7 @@ ng = d[:, 6].sum()
 names = ["tail/back-edge", "staging issue", "staging wait", "prologue compute", "horizon loop", "epilogue"]
 order = [5, 0, 1, 2, 3, 4]
 tot = d[:, :6].sum()
-print(f"p={p}: {len(d)} waves, {ng:.0f} groups; s_memtime cycles per group:")
+print(f"{KERNEL} kernel, {PLANT}-{CTYPE} p={p}: {len(d)} waves, {ng:.0f} groups; s_memtime cycles per group:")
 for i in order:
     print(f"  {names[order.index(i)] if False else ['staging issue','staging wait','prologue compute','horizon loop','epilogue','tail/back-edge'][i]:18s} {d[:, i].sum() / ng:10.0f}  ({d[:, i].sum() / tot * 100:5.1f} %)")
 clk = d[:, 8] / (d[:, 9] / 100e6) / 1e9
