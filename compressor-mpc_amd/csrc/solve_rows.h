@@ -22,10 +22,19 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
   const bool own = l < N;
   const double* cfg = P.cfg + (size_t)s * P.co.len;
 
+  // every global operand is requested before the first wait (small batches
+  // leave one wave per SIMD: the H^-1 factorisation's LDS barriers would
+  // otherwise expose one HBM round trip per load group)
   RowQp<N, NU> qp;
   double uo[NU];
 #pragma unroll
   for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
+  uint32_t ws = P.ws[q];
+  double dprev[N];  // (without other controllers only the K = 0 output reads it)
+  if constexpr (NVO > 0) {
+#pragma unroll
+    for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+  }
 #pragma unroll
   for (int c = 0; c < NU; ++c) {
     qp.lb[c] = cfg[P.co.lower + c] - uo[c];
@@ -45,7 +54,6 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
   }
   const double tol_d = TOL_D * (1.0 + hmax);
 
-  uint32_t ws = P.ws[q];
   double x[N];
   QpOut o;
   if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
@@ -53,9 +61,10 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
     if (active && l == 0) P.ws[q] = o.ws;
     return;
   }
-  double dprev[N];
+  if constexpr (NVO == 0) {
 #pragma unroll
-  for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+    for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+  }
   for (int k = 0; k < P.K; ++k) {
     {  // fair progress of the SIMD's waves (cf. cmpc_solve_kernel)
       const int level = 3 - (4 * k) / (P.K > 0 ? P.K : 1);
