@@ -702,10 +702,8 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPG, lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
+  int per_cu = cmpc_blocks_per_cu(kern, 64 * WPG, lds);
+  if (per_cu < 1) per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   per_cu = std::min(per_cu, std::max(1, 4 * WPE / WPG));  // the register budget's waves per SIMD
   // the occupancy query counts the requested LDS only; the measured
   // allocation model (rows_layout.cpp) can allow fewer

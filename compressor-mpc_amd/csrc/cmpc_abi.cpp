@@ -75,6 +75,7 @@ namespace {
 // the copies that read the buffer, and the next writer waits on it.
 struct PinnedIO {
   char* buf = nullptr;
+  char* dev = nullptr;  // the device's address of buf (kernels read it in place)
   size_t cap = 0;
   hipEvent_t busy = nullptr;
   bool pending = false;
@@ -90,8 +91,11 @@ int pinned_acquire(PinnedIO& p, size_t bytes) {
     p.buf = nullptr;
     p.cap = 0;
     const size_t cap = std::max<size_t>(bytes, 4096);
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p.buf), cap, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p.buf), cap, hipHostMallocCoherent));
     p.cap = cap;
+    void* dv = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dv, p.buf, 0));
+    p.dev = reinterpret_cast<char*>(dv);
   }
   return 0;
 }
@@ -111,7 +115,10 @@ void pinned_free(PinnedIO& p) {
 }
 
 // host -> device: the k arrays (nullptr skipped) are packed into `pin` and
-// copied by one DMA to `dev_base`; dev[i] receives each array's device address
+// copied by one DMA to `dev_base`; dev[i] receives each array's device address.
+// dev_base == nullptr: no copy, the kernels read the page-locked buffer in
+// place (dev[i] = its device address) and the caller calls pinned_release
+// after the launch that reads it.
 constexpr size_t kPad = 2;  // keep every array 16-byte aligned
 int pinned_upload(PinnedIO& pin, hipStream_t s, double* dev_base, const double* const* host,
                   const size_t* n, int k, const double** dev) {
@@ -124,9 +131,10 @@ int pinned_upload(PinnedIO& pin, hipStream_t s, double* dev_base, const double* 
     if (dev) dev[i] = nullptr;
     if (!host[i]) continue;
     std::memcpy(h + off, host[i], sizeof(double) * n[i]);
-    if (dev) dev[i] = dev_base + off;
+    if (dev) dev[i] = (dev_base ? dev_base : reinterpret_cast<double*>(pin.dev)) + off;
     off += (n[i] + kPad - 1) / kPad * kPad;
   }
+  if (!dev_base) return 0;
   if (off) HIP_TRY(hipMemcpyAsync(dev_base, h, sizeof(double) * off, hipMemcpyHostToDevice, s));
   return pinned_release(pin, s);
 }
@@ -157,6 +165,7 @@ struct cmpc_ctx {
   uint32_t* own_ws = nullptr;
   int32_t *status = nullptr, *nwsr = nullptr, *ntrace = nullptr;
   char* out_block = nullptr;  // du | status | nwsr in one allocation: one D2H for cmpc_download
+  bool out_host = false;      // out_block is page-locked host memory the kernels write in place
   size_t out_st = 0, out_nw = 0, out_len = 0;  // byte offsets of status, nwsr; block length
   uint8_t* trace = nullptr;
   size_t trace_cap = 0;
@@ -428,20 +437,34 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
     c->out_st = up16(sizeof(double) * n * L.nV);
     c->out_nw = c->out_st + up16(sizeof(int32_t) * n);
     c->out_len = c->out_nw + sizeof(int32_t) * n;
-    if (hipMalloc(&c->out_block, c->out_len) != hipSuccess)
-      return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
-    c->du = reinterpret_cast<double*>(c->out_block);
-    c->status = reinterpret_cast<int32_t*>(c->out_block + c->out_st);
-    c->nwsr = reinterpret_cast<int32_t*>(c->out_block + c->out_nw);
+    // a few QPs (the reference's own B = 1 call pattern): the kernels write
+    // du, status and nWSR straight into page-locked host memory, so
+    // cmpc_download is a stream sync, no copy (a hipMemcpyAsync cost ~7 us of
+    // host time and a copy kernel per step, profiles/r4e_b1_hip_api_stats.csv)
+    char* dev_out = nullptr;
+    if (n <= CMPC_HOST_OUT_MAX_QP) {
+      void* dv = nullptr;
+      if (hipHostMalloc(reinterpret_cast<void**>(&c->out_block), c->out_len, hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer(&dv, c->out_block, 0) != hipSuccess)
+        return cleanup(fail("hipHostMalloc failed"));
+      c->out_host = true;
+      std::memset(c->out_block, 0, c->out_len);
+      dev_out = reinterpret_cast<char*>(dv);
+    } else {
+      if (hipMalloc(&c->out_block, c->out_len) != hipSuccess)
+        return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
+      dev_out = c->out_block;
+    }
+    c->du = reinterpret_cast<double*>(dev_out);
+    c->status = reinterpret_cast<int32_t*>(dev_out + c->out_st);
+    c->nwsr = reinterpret_cast<int32_t*>(dev_out + c->out_nw);
   }
   if (hipMemsetAsync(c->lin, 0, sizeof(double) * n * L.rec_len, c->stream) != hipSuccess ||
       hipMemsetAsync(c->qp, 0, sizeof(double) * n * c->qp_len, c->stream) != hipSuccess ||
       hipMemsetAsync(c->u_old, 0, sizeof(double) * n * d.nu_tot, c->stream) != hipSuccess ||
       hipMemsetAsync(c->du_old, 0, sizeof(double) * n * L.nV, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->du, 0, sizeof(double) * n * L.nV, c->stream) != hipSuccess ||
+      (!c->out_host && hipMemsetAsync(c->out_block, 0, c->out_len, c->stream) != hipSuccess) ||
       hipMemsetAsync(c->ws, 0, sizeof(uint32_t) * n, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->status, 0, sizeof(int32_t) * n, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->nwsr, 0, sizeof(int32_t) * n, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return cleanup(fail("device initialisation failed"));
   *out = c;
@@ -462,10 +485,11 @@ int cmpc_destroy(cmpc_ctx* c) {
   pinned_free(c->pin_out);
   // own state buffers (bound external ones belong to the caller); before they
   // are recorded (a failed create) the active pointers are the own ones
+  if (c->out_host && c->out_block) (void)hipHostFree(c->out_block);
   void* bufs[] = {c->lin, c->qp, c->cfg,
                   c->own_u_old ? c->own_u_old : c->u_old,
                   c->own_du_old ? c->own_du_old : c->du_old,
-                  c->out_block,
+                  c->out_host ? nullptr : c->out_block,
                   c->own_ws ? c->own_ws : c->ws,
                   c->trace, c->ntrace, c->obs, c->d_obsM,
                   c->stage};
@@ -876,11 +900,14 @@ int cmpc_observe_apply(cmpc_ctx* c) {
 
 // copies host arrays (nullptr entries skipped) into the context's staging
 // buffer on its stream; returns their device addresses
+// host arrays of up to this many doubles are read by the kernels in place
+static bool stage_in_place(size_t tot) { return tot <= 1024; }
+
 static int stage_host(cmpc_ctx* c, const double* const* host, const size_t* n, int k,
                       const double** dev) {
   size_t tot = 0;
   for (int i = 0; i < k; ++i) tot += host[i] ? (n[i] + 1) / 2 * 2 : 0;
-  if (tot > c->stage_cap) {
+  if (!stage_in_place(tot) && tot > c->stage_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->stage) HIP_TRY(hipFree(c->stage));
     c->stage = nullptr;
@@ -888,8 +915,14 @@ static int stage_host(cmpc_ctx* c, const double* const* host, const size_t* n, i
     c->stage_cap = tot;
   }
   // one DMA from page-locked memory (the device stage is read by kernels
-  // queued after the copy on the same stream)
-  return pinned_upload(c->pin_in, c->stream, c->stage, host, n, k, dev);
+  // queued after the copy on the same stream); small arrays are read by the
+  // kernel in place (no copy: the caller releases the buffer after the launch)
+  return pinned_upload(c->pin_in, c->stream, stage_in_place(tot) ? nullptr : c->stage, host, n, k, dev);
+}
+
+// after the launch that reads what stage_host staged
+static int stage_done(cmpc_ctx* c) {
+  return c->pin_in.pending ? 0 : pinned_release(c->pin_in, c->stream);
 }
 
 int cmpc_observer_init_host(cmpc_ctx* c, int plant, double p_in, double p_out, double Ts,
@@ -905,7 +938,8 @@ int cmpc_observer_init_host(cmpc_ctx* c, int plant, double p_in, double p_out, d
   const size_t n[4] = {B * ns, B * ni, B * no, (size_t)c->nqp * c->L.ntot};
   const double* d[4];
   if (stage_host(c, h, n, 4, d)) return -1;
-  return cmpc_observer_init(c, plant, p_in, p_out, Ts, input_order, out_idx, d[0], d[1], d[2], d[3]);
+  const int rc = cmpc_observer_init(c, plant, p_in, p_out, Ts, input_order, out_idx, d[0], d[1], d[2], d[3]);
+  return stage_done(c) ? -1 : rc;
 }
 
 int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
@@ -919,7 +953,8 @@ int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
   const size_t n[2] = {B * ni, B * no};
   const double* d[2];
   if (stage_host(c, h, n, 2, d)) return -1;
-  return cmpc_observe_step(c, d[0], d[1]);
+  const int rc = cmpc_observe_step(c, d[0], d[1]);
+  return stage_done(c) ? -1 : rc;
 }
 
 // ---- plant simulation ----
@@ -1585,7 +1620,8 @@ int cmpc_get_input_host(cmpc_ctx* c, const double* du_last, uint32_t flags) {
   const size_t n[1] = {(size_t)c->nqp * c->L.nVo};
   const double* d[1];
   if (stage_host(c, h, n, 1, d)) return -1;
-  return cmpc_get_input(c, d[0], flags);
+  const int rc = cmpc_get_input(c, d[0], flags);
+  return stage_done(c) ? -1 : rc;
 }
 
 // DistributedController::UpdateU(du) (include/distributed_controller.h:145-152)
@@ -1614,7 +1650,8 @@ int cmpc_update_u_host(cmpc_ctx* c, const double* du_full) {
   const size_t n[1] = {(size_t)c->nqp * c->d.nu_tot};
   const double* d[1];
   if (stage_host(c, h, n, 1, d)) return -1;
-  return cmpc_update_u(c, d[0]);
+  const int rc = cmpc_update_u(c, d[0]);
+  return stage_done(c) ? -1 : rc;
 }
 
 int cmpc_coupled_validate(const cmpc_dims* d, int S_total, int S_local, int s_offset, size_t G_ext_len,
@@ -1702,15 +1739,13 @@ int cmpc_last_step_fused(cmpc_ctx* c) {
 int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   if (!c) return fail("null context");
   if (K < 0) return fail("K must be >= 0");
-  // AUTO fuses small batches where the fused kernel is the build kernel AUTO
-  // would pick anyway: the one-QP-per-wave kernel for centralized batches
-  // under one row group per SIMD (SURVEY config 5: 43.9 vs 46.1 us per step),
-  // the row kernel from one row group per SIMD up (config 2: 36.0 vs
-  // 37.8 us); a coop batch under 4 096 QPs stays split (wave build + lane
-  // solve: B = 1 28.2 vs 33.1 us fused on the row kernel)
+  // AUTO fuses small batches on the build kernel AUTO would pick anyway: the
+  // one-QP-per-wave kernel under one row group per SIMD (its own row solver
+  // for centralized QPs, SURVEY config 5: 40.1 vs 44.8 us per step; the lane
+  // solver of wave 0 after a workgroup barrier for S = 2, 4), the row kernel
+  // from one row group per SIMD up to 16 384 QPs (config 2)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const bool rows_fill_ = (c->nqp + 3) / 4 >= 4 * (c->cus > 0 ? c->cus : 256);
-  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && (c->d.S == 1 ? !rows_fill_ : rows_fill_);
+  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP;
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
                     (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);
@@ -1731,21 +1766,21 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
     if (tl.begin()) return -1;
     const cmpc_dims& d = c->d;
     // the build kernel AUTO would pick: one QP per wave below one row group per
-    // SIMD (centralized only, S = 1), else four QPs per wave
+    // SIMD, else four QPs per wave
     const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
-    int rc = -1, kind = CMPC_BUILD_ROWS;
-    if (d.S == 1 && !rows_fill) {
-      rc = cmpc_launch_step_wave(P, d.ns, d.ny, d.nu, d.m, c->stream);
+    int rc = -1, kind = CMPC_BUILD_ROWS, solver = CMPC_SOLVE_ROWS;
+    if (!rows_fill) {
+      rc = cmpc_launch_step_wave(P, d.ns, d.ny, d.nu, d.m, c->stream, &solver);
       kind = CMPC_BUILD_WAVE;
     }
     if (rc) {
-      rc = cmpc_launch_step_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
+      rc = cmpc_launch_step_rows(P, d.ns, d.ny, d.nu, d.m, c->stream, &solver);
       kind = CMPC_BUILD_ROWS;
     }
     if (rc == 0) {
       if (check_launch("fused step kernel")) return -1;
       c->last_build = kind;
-      c->last_solve = CMPC_SOLVE_ROWS;
+      c->last_solve = solver;
       c->last_step_fused = 1;
       return tl.end();
     }
@@ -1771,6 +1806,13 @@ int cmpc_download(cmpc_ctx* c, double* du, int32_t* status, int32_t* nwsr) {
   const size_t n = (size_t)c->nqp;
   const size_t b_du = sizeof(double) * n * c->L.nV, b_i = sizeof(int32_t) * n;
   const size_t o_st = c->out_st, o_nw = c->out_nw;
+  if (c->out_host) {  // the kernels wrote the block in place
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (du) std::memcpy(du, c->out_block, b_du);
+    if (status) std::memcpy(status, c->out_block + o_st, b_i);
+    if (nwsr) std::memcpy(nwsr, c->out_block + o_nw, b_i);
+    return 0;
+  }
   // device -> page-locked buffer (DMA; one copy of the du | status | nwsr
   // block when all are asked for), then host copies after one sync
   if (pinned_acquire(c->pin_out, c->out_len)) return -1;

@@ -19,8 +19,36 @@ struct LaunchEvents {
 extern thread_local LaunchEvents cmpc_launch_events;
 template <typename F, typename... A>
 inline void cmpc_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t stream, A... args) {
-  hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, stream, cmpc_launch_events.start,
-                        cmpc_launch_events.stop, 0u, args...);
+  if (cmpc_launch_events.start || cmpc_launch_events.stop)
+    hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, stream, cmpc_launch_events.start,
+                          cmpc_launch_events.stop, 0u, args...);
+  else  // the plain launch path: ~8 us of host time per hipExtLaunchKernel
+        // call in the B = 1 step's --hip-trace (profiles/r4e_b1_hip_api_stats.csv)
+    hipLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, stream, args...);
+}
+
+// Resident workgroups per CU of `kernel` at `threads` x `lds` bytes, from the
+// occupancy query, cached per (kernel, threads, lds): the query costs ~9 us of
+// host time per call (B = 1 step --hip-trace), once per launch before.
+// 0 when the query fails.  One context per host thread, hence thread_local.
+template <typename F>
+inline int cmpc_blocks_per_cu(F kernel, int threads, size_t lds) {
+  struct Entry {
+    const void* k;
+    int threads;
+    size_t lds;
+    int blocks;
+  };
+  static thread_local Entry cache[32];
+  static thread_local int n = 0;
+  const void* key = reinterpret_cast<const void*>(kernel);
+  for (int i = 0; i < n && i < 32; ++i)
+    if (cache[i].k == key && cache[i].threads == threads && cache[i].lds == lds) return cache[i].blocks;
+  int v = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, threads, lds) != hipSuccess) v = 0;
+  cache[n % 32] = Entry{key, threads, lds, v};
+  ++n;
+  return v;
 }
 
 #define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
@@ -31,6 +59,7 @@ inline void cmpc_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t
 #define CMPC_ROWS_NSEG 16        // loop segment bounds of the row build kernel
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 #define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
+#define CMPC_HOST_OUT_MAX_QP 64  // up to this many QPs: du/status/nWSR live in page-locked host memory
 #ifndef CMPC_SOLVE_ROWS_MAX_QP
 #define CMPC_SOLVE_ROWS_MAX_QP 16384  // CMPC_SOLVE_AUTO: the row solve kernel below this many QPs
 #endif
@@ -210,11 +239,12 @@ int cmpc_launch_build(const BuildParams& P, int ns, int ny, int nu, int m,
 // Row-layout build kernel (build_rows.hip); -1 when not instantiated / not usable.
 int cmpc_launch_build_rows(const BuildParams& P, int ns, int ny, int nu, int m,
                            void* stream);
-// Fused step (build_rows.hip): the row build kernel running the K Jacobi
-// iterations of its QPs itself (P.sv); -1 when not available.
-int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream);
-// the same on the one-QP-per-wave build kernel (cmpc_kernels.hip; S = 1)
-int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream);
+// Fused step (step_rows.hip): the row build kernel running the K Jacobi
+// iterations of its QPs itself (P.sv); -1 when not available.  *solver:
+// the solver it runs (CMPC_SOLVE_ROWS or CMPC_SOLVE_LANE).
+int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream, int* solver);
+// the same on the one-QP-per-wave build kernel (cmpc_kernels.hip)
+int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream, int* solver);
 // Waves per workgroup the row kernel launches with for layout R (4, 2 or 1;
 // 0: does not fit) (build_rows.hip).
 int cmpc_rows_waves_per_group(const RowsLayout& R);

@@ -29,6 +29,7 @@
 #include "cmpc_internal.h"
 #include "dpp_blocks.inc"
 #include "solve_rows.h"
+#include "lane_solve.h"
 
 // Ablation switches for timing experiments (tools/ablate.sh); the product
 // build uses CMPC_EXP = 0.
@@ -58,6 +59,7 @@
 #ifndef CMPC_BUILD_ILP
 #define CMPC_BUILD_ILP 1
 #endif
+
 #if CMPC_BUILD_ILP == 4
 #define CMPC_ILP_PROP(pv, m, ax) prop4w_dpp<NS, ND>(pv, m, ax)
 #define CMPC_ILP_SUM(ax) (((ax)[0] + (ax)[1]) + ((ax)[2] + (ax)[3]))
@@ -128,10 +130,14 @@
 // ---------------------------------------------------------------------------
 // build kernel
 // ---------------------------------------------------------------------------
-// FUSE (cmpc_step on small centralized batches, S = 1): after a QP is built
-// its wave runs the K Jacobi iterations on it (solve_rows.h: row 0 is the
-// QP's solver row, rows 1-3 shadow it without stores); 1 plain, 2 with the
-// working-set trace.  The QP is still stored (cmpc_download_qp).
+// FUSE (cmpc_step on small batches, one QP per wave): 1/2 (centralized,
+// S = 1): after a QP is built its wave runs the K Jacobi iterations on it
+// (solve_rows.h: row 0 is the QP's solver row, rows 1-3 shadow it without
+// stores); 3/4 (S divides 4, nV <= 4): the workgroup's QPs, built and stored
+// one per wave, are solved one per lane of wave 0 after a workgroup barrier
+// (lane_solve.h; a scenario's sub-controllers are adjacent waves, so adjacent
+// lanes).  Even FUSE values record the working-set trace.  The QP is stored
+// either way (cmpc_download_qp).
 template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE = 0>
 __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES)
 __attribute__((amdgpu_waves_per_eu(FUSE ? 1 : 4, FUSE ? 1 : 4)))
@@ -506,7 +512,7 @@ void cmpc_build_kernel(BuildParams P) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) red_w[k] = acc[k];
     }
-    if constexpr (FUSE > 0) {
+    if constexpr (FUSE == 1 || FUSE == 2) {
       // every row forms the totals (row 0's partial through LDS as well), in
       // the order row 0 uses below: the solver's four rows see the same H
       if (row == 0 && col < NG) {
@@ -600,6 +606,21 @@ void cmpc_build_kernel(BuildParams P) {
     __builtin_amdgcn_wave_barrier();
     CMPC_WT(4)  // epilogue
   }
+  if constexpr (FUSE >= 3) {
+    // every wave has stored its QP (one per wave: the launcher's grid covers
+    // the batch); the barrier's workgroup-scope release/acquire makes the
+    // stores of the other waves visible to wave 0 (one CU, write-through L0)
+    __syncthreads();
+    if (wave == 0 && lane < CMPC_BUILD_WAVES) {
+      constexpr int NVO = M * (NUT - NU);
+      const int ql = blockIdx.x * CMPC_BUILD_WAVES + lane;
+      const bool al = ql < P.nqp;
+      const int qc = al ? ql : P.nqp - 1;
+      const int sl = qc % S;
+      const double* qr = P.qp + (size_t)qc * P.qp_len;
+      lane_solve_qp<NV, NU, NVO, FUSE == 4, false, 1>(P.sv, qc, al, sl, lane - sl, qr, qr + NV * NV + NV);
+    }
+  }
 #if CMPC_WAVE_TIMING
   // slots as CMPC_ROWS_TIMING: 0 staging, 1 fused solve, 2 prologue, 3 loop,
   // 4 epilogue, 5 back-edge; 6 QPs, 7 marker, 8-11 clocks, 12-14 placement
@@ -619,8 +640,6 @@ void cmpc_build_kernel(BuildParams P) {
   }
 #endif
 }
-
-#include "lane_solve.h"
 
 #ifndef CMPC_SOLVE_WPE
 #define CMPC_SOLVE_WPE(N) ((N) >= 6 ? 1 : 2)
@@ -721,19 +740,17 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
       (void)hipFuncSetAttribute(                                                       \
           reinterpret_cast<const void*>(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>),   \
           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
-    int per_cu = 0;                                                                    \
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                 \
-            &per_cu, cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>, 64 * CMPC_BUILD_WAVES,  \
-            lds) != hipSuccess || per_cu < 1)                                         \
-      per_cu = std::max<int>(1, (int)((160 * 1024) / lds));                            \
+    int per_cu = cmpc_blocks_per_cu(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>,        \
+                                    64 * CMPC_BUILD_WAVES, lds);                       \
+    if (per_cu < 1) per_cu = std::max<int>(1, (int)((160 * 1024) / lds));             \
     const int grid = std::max(1, std::min(P.grid, P.cus * per_cu));                   \
     cmpc_launch((cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>), dim3(grid),                  \
                 dim3(64 * CMPC_BUILD_WAVES), lds, s, P);                               \
     return 0;                                                                          \
   }
 
-// fused build + K iterations on the one-QP-per-wave kernel (S = 1 only: the
-// plan exchange of S > 1 would cross waves)
+// fused build + K iterations on the one-QP-per-wave kernel, row solver in
+// the QP's own wave (S = 1)
 #define STEP_WAVE_CASE(NS_, NY_, NU_, M_)                                                \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {   \
     if (P.lds_per_wave < NY_ * (M_ * 4 + 1) * (NU_ * M_) + 4 * (NU_ * M_) * (NU_ * M_)) \
@@ -756,13 +773,38 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
     return 0;                                                                            \
   }
 
+// the same with the lane solver after a workgroup barrier (S divides 4, the
+// scenario's sub-controllers in adjacent waves of one workgroup)
+#define STEP_WAVE_LANE_CASE(NS_, NY_, NU_, M_)                                           \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {   \
+    const size_t lds = sizeof(double) * ((size_t)P.lds_block +                           \
+                                         (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);    \
+    auto k_ = P.sv.trace ? cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 4>                 \
+                         : cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 3>;                \
+    if (lds > 64 * 1024)                                                                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);   \
+    *solver = CMPC_SOLVE_LANE;                                                           \
+    cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P);   \
+    return 0;                                                                            \
+  }
+
 // one workgroup per four QPs (no persistent loop: the fused path is for
-// batches that give fewer waves than the GPU holds)
-int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
+// batches that give fewer waves than the GPU holds, each wave one QP)
+int cmpc_launch_step_wave(const BuildParams& P, int ns, int ny, int nu, int m, void* stream, int* solver) {
   hipStream_t s = (hipStream_t)stream;
-  if (P.S != 1) return -1;
-  STEP_WAVE_CASE(11, 3, 4, 2)  // parallel centralized
-  STEP_WAVE_CASE(10, 4, 4, 2)  // serial centralized
+  if (P.grid * CMPC_BUILD_WAVES < P.nqp) return -1;
+  if (P.S == 1) {
+    *solver = CMPC_SOLVE_ROWS;
+    STEP_WAVE_CASE(11, 3, 4, 2)  // parallel centralized
+    STEP_WAVE_CASE(10, 4, 4, 2)  // serial centralized
+    return -1;
+  }
+  if (CMPC_BUILD_WAVES % P.S) return -1;
+  STEP_WAVE_LANE_CASE(11, 3, 2, 2)  // parallel coop
+  STEP_WAVE_LANE_CASE(11, 2, 2, 2)  // parallel ncoop
+  STEP_WAVE_LANE_CASE(10, 2, 2, 2)  // serial ncoop
+  STEP_WAVE_LANE_CASE(10, 4, 2, 2)  // serial coop
   return -1;
 }
 

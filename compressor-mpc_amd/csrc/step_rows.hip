@@ -11,6 +11,7 @@
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
     if (cmpc_rows_waves_per_group(P.rows) != 4) return -1;                           \
     if (P.rows.per_wave < 4 * (NU_ * M_) * (NU_ * M_)) return -1;                    \
+    *solver = CMPC_SOLVE_ROWS;                                                         \
     if (ring) {                                                                        \
       if (trace) return rows_launch<NS_, NY_, NU_, M_, 4, true, 1, 2>(P, s);          \
       return rows_launch<NS_, NY_, NU_, M_, 4, true, 1, 1>(P, s);                     \
@@ -25,11 +26,12 @@
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
     if (cmpc_rows_waves_per_group(P.rows) != 4 || ring) return -1;                   \
     if ((P.nqp + 3) / 4 > 16 * 4 * P.cus) return -1;                                 \
+    *solver = CMPC_SOLVE_LANE;                                                         \
     if (trace) return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 4>(P, s);           \
     return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 3>(P, s);                      \
   }
 
-int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream) {
+int cmpc_launch_step_rows(const BuildParams& P, int ns, int ny, int nu, int m, void* stream, int* solver) {
   hipStream_t s = (hipStream_t)stream;
   if (!P.rows.ok || P.S < 1 || 4 % P.S) return -1;
   bool ring = false;

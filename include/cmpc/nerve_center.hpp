@@ -798,8 +798,7 @@ class NerveCenter : public ControllerInterface {
     for (int c = 0; c < spec_.nu_tot; ++c) u_full[spec_.plant_input_index[c]] += u_old_[c];
     // ObserveAPosteriori + Update at each sub-controller's estimate
     Check(cmpc_observe_step_host(ctx_, u_full.data(), y), "cmpc_observe_step_host");
-    Check(cmpc_build(ctx_), "cmpc_build");
-    const int64_t stopped = Iterate(n_timing_iterations, 0u);
+    const int64_t stopped = Step(n_timing_iterations, 0u);
     Download();
     // UpdateU of every sub-controller (observer a priori + its u_old_)
     Check(cmpc_observe_apply(ctx_), "cmpc_observe_apply");
@@ -826,8 +825,7 @@ class NerveCenter : public ControllerInterface {
     for (int c = 0; c < spec_.nu_tot; ++c) u_full[spec_.plant_input_index[c]] += u_old_[c];
     FillRecords(x_hat, u_full.data(), dx_aug, y);
     Check(cmpc_upload_lin(ctx_, rec_.data()), "cmpc_upload_lin");
-    Check(cmpc_build(ctx_), "cmpc_build");
-    const int64_t stopped = Iterate(n_timing_iterations, CMPC_APPLY_MOVE);
+    const int64_t stopped = Step(n_timing_iterations, CMPC_APPLY_MOVE);
     Download();
     return Finish(stopped, t0, time_out_ns);
   }
@@ -850,8 +848,12 @@ class NerveCenter : public ControllerInterface {
   // K Jacobi iterations, the last with `last_flags`.  If 0 <= n < K, the
   // reference stops its timer before iteration n and resumes it after the
   // loop (nerve_center.h:151,158): returns that stopped span (ns), else 0.
-  int64_t Iterate(int n_timing_iterations, uint32_t last_flags) {
+  // build + K Jacobi iterations: one cmpc_step (a single fused launch for
+  // small batches), or, when the timing stops at iteration n, the build and
+  // the first n iterations, then the untimed rest
+  int64_t Step(int n_timing_iterations, uint32_t last_flags) {
     if (n_timing_iterations >= 0 && n_timing_iterations < K_) {
+      Check(cmpc_build(ctx_), "cmpc_build");
       Check(cmpc_iterate(ctx_, n_timing_iterations, 0u), "cmpc_iterate");
       Check(cmpc_synchronize(ctx_), "cmpc_synchronize");
       const auto stop = std::chrono::steady_clock::now();
@@ -860,7 +862,12 @@ class NerveCenter : public ControllerInterface {
       return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - stop)
           .count();
     }
-    Check(cmpc_iterate(ctx_, K_, last_flags), "cmpc_iterate");
+    if (K_ > 0) {
+      Check(cmpc_step(ctx_, K_, last_flags), "cmpc_step");
+    } else {
+      Check(cmpc_build(ctx_), "cmpc_build");
+      Check(cmpc_iterate(ctx_, 0, last_flags), "cmpc_iterate");
+    }
     return 0;
   }
   void Download() {

@@ -95,12 +95,12 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
 
 @pytest.mark.parametrize("ctype,B,solve,fused", [
     ("cent", 16, cmpc.CMPC_SOLVE_ROWS, True), ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
-    ("coop", 1, cmpc.CMPC_SOLVE_LANE, False), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, True),
+    ("coop", 1, cmpc.CMPC_SOLVE_LANE, True), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, True),
     ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
 def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
     """CMPC_SOLVE_AUTO: the row solve kernel for small nV = 8 batches only;
-    CMPC_STEP_AUTO: cmpc_step fused for small centralized batches and for
-    coop batches of one row group per SIMD up to 16 384 QPs."""
+    CMPC_STEP_AUTO: cmpc_step fused below 16 384 QPs (the one-QP-per-wave
+    kernel under one row group per SIMD, the row kernel above)."""
     cfg = cmpc.reference_config("par", ctype, p=20)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", ctype))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
@@ -114,11 +114,14 @@ def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
         assert ctx.last_solve_kernel() == solve
         ctx.step(2)
         assert ctx.last_step_fused() == fused
+        if fused:  # the fused kernel reports the solver it ran
+            assert ctx.last_solve_kernel() == solve
 
 
 FUSED_CASES = [  # plant, controller, p, K, B scenarios (the kernel AUTO fuses on)
-    ("par", "coop", 20, 9, 4096),     # SURVEY config 2: the row build kernel
-    ("par", "coop", 20, 9, 13),
+    ("par", "coop", 20, 9, 4096),     # SURVEY config 2: the row build kernel, lane solver
+    ("par", "cent", 20, 1, 8192),     # the row build kernel, row solver per group
+    ("par", "coop", 20, 9, 13),       # one-QP-per-wave kernel, lane solver of wave 0
     ("par", "coop", 50, 9, 1),        # B = 1, the reference's own call pattern
     ("par", "ncoop", 50, 9, 64),
     ("par", "cent", 200, 1, 1024),    # SURVEY config 5: the one-QP-per-wave kernel
