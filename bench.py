@@ -353,6 +353,29 @@ def cpp_step_latency(plant, ctype, p, steps=400):
     return out
 
 
+def run_configs(local, settle_seconds, steps, with_cpp=True):
+    """SURVEY §8(d) / BASELINE.json configs 2, 3 and 5 at their batch sizes on
+    this GPU, and (with_cpp) config 1 and the coop-par B = 1 step through the
+    C++ adapter; each entry failure-tolerant."""
+    configs = {}
+    for key, (pl, ct, p_, B_, K_) in {"2": ("par", "coop", 20, 4096, 9),
+                                     "3": ("par", "ncoop", 50, 65536, 1),
+                                     "5": ("par", "cent", 200, 1024, 1)}.items():
+        try:
+            configs[key] = time_config(key, pl, ct, p_, B_, K_, local, settle_seconds, max(20, steps))
+        except Exception as e:  # reported, never required
+            log(f"config {key} failed: {e}")
+            configs[key] = {"error": str(e)[:300]}
+    if with_cpp:
+        for key, (pl, ct, p_) in {"1": ("ser", "cent", 100), "b1_coop_par": ("par", "coop", 50)}.items():
+            try:
+                configs[key] = cpp_step_latency(pl, ct, p_)
+            except Exception as e:  # reported, never required
+                log(f"config {key} failed: {e}")
+                configs[key] = {"error": str(e)[:300]}
+    return configs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -372,6 +395,9 @@ def main():
                     help="only the metric's steps (no K = 1, closed-loop, coupled or CPU sections): "
                          "profiler runs, so that every build launch in the trace is a headline one")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
+    ap.add_argument("--configs-only", action="store_true",
+                    help="only the SURVEY-config section's GPU configs (2, 3, 5), one JSON line: "
+                         "profiler runs, so that the kernel statistics are the configs' own")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the SURVEY-config section (configs 1, 2, 3, 5 on this GPU)")
     ap.add_argument("--coupled-batch", type=int, default=4096, help="config-4 scenarios per GPU")
@@ -404,6 +430,11 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+
+    if args.configs_only:
+        print(json.dumps({"configs": run_configs(local, args.settle_seconds, args.steps, with_cpp=False)}),
+              flush=True)
+        return
 
     import cmpc
     from cmpc.configs import reference_setup
@@ -778,22 +809,7 @@ def main():
     # adapter, 2, 3 and 5 at their batch sizes; 4 is the `coupled` section
     configs = None
     if not args.no_configs and not args.headline_only and world == 1:
-        configs = {}
-        for key, (pl, ct, p_, B_, K_) in {"2": ("par", "coop", 20, 4096, 9),
-                                         "3": ("par", "ncoop", 50, 65536, 1),
-                                         "5": ("par", "cent", 200, 1024, 1)}.items():
-            try:
-                configs[key] = time_config(key, pl, ct, p_, B_, K_, local, args.settle_seconds,
-                                           max(20, args.steps))
-            except Exception as e:  # reported, never required
-                log(f"config {key} failed: {e}")
-                configs[key] = {"error": str(e)[:300]}
-        for key, (pl, ct, p_) in {"1": ("ser", "cent", 100), "b1_coop_par": ("par", "coop", 50)}.items():
-            try:
-                configs[key] = cpp_step_latency(pl, ct, p_)
-            except Exception as e:  # reported, never required
-                log(f"config {key} failed: {e}")
-                configs[key] = {"error": str(e)[:300]}
+        configs = run_configs(local, args.settle_seconds, args.steps)
     coupled, rc, el_c = None, None, float("inf")
     if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench

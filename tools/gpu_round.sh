@@ -11,6 +11,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 900 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --headline-only > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
+# the SURVEY configs' own kernels (no headline launches in this trace): their
+# --stats averages against the configs section of the bench line above
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfgprof_$TAG -o run --output-format csv -- python3 bench.py --configs-only --no-cpu > gpurun_out/cfgprof_$TAG.json 2> gpurun_out/cfgprof_$TAG.err || exit $?
 pmc() {  # name, counters...   (separate passes, kernel trace only)
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace -T --kernel-include-regex 'cmpc_' \

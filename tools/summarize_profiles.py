@@ -4,6 +4,8 @@
 usage: python tools/summarize_profiles.py TAG ROUND [BATCH]
 
   gpurun_out/prof_TAG/run_kernel_stats.csv      -> profiles/ROUND_kernel_stats.csv
+  gpurun_out/cfgprof_TAG/run_kernel_stats.csv   -> profiles/ROUND_configs_kernel_stats.csv
+                                                 (+ that run's configs line)
   gpurun_out/pmcTAG_{sq1,sq2,fetch,write}/...   -> profiles/ROUND_pmc.json
                                                  + profiles/pmc_build_coop_p50.json
 
@@ -51,6 +53,11 @@ def main():
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(PROF, f"{rnd}_kernel_stats.csv"))
         print("copied", ks)
+    cs = os.path.join(OUT, f"cfgprof_{tag}", "run_kernel_stats.csv")
+    if os.path.exists(cs):  # bench.py --configs-only under rocprofv3 --stats
+        shutil.copy(cs, os.path.join(PROF, f"{rnd}_configs_kernel_stats.csv"))
+        shutil.copy(os.path.join(OUT, f"cfgprof_{tag}.json"), os.path.join(PROF, f"{rnd}_configs_bench.json"))
+        print("copied", cs)
     merged = defaultdict(dict)
     for name in ("sq1", "sq2", "fetch", "write"):
         for k, d in counters(tag, name).items():
