@@ -207,7 +207,7 @@ def main():
                 if mm * nut + 1 <= 16 and nu * mm <= 8:
                     parts.append(gacc(nut, nu, mm))
     # fused chain + gather accumulation for the instantiated build kernels
-    for ns, nd, nut, nu, mm in [(11, 2, 4, 2, 2), (11, 2, 4, 4, 2), (10, 2, 4, 2, 2),
+    for ns, nd, nut, nu, mm in [(11, 2, 4, 2, 2), (11, 2, 4, 4, 2), (10, 2, 4, 2, 2), (10, 2, 4, 4, 2),
                                 (11, 2, 4, 2, 1), (11, 2, 4, 2, 3)]:
         parts.append(prop1w_gacc(ns, nd, nut, nu, mm))
     with open(OUT, "w") as fh:
