@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -417,6 +418,10 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
     cmpc_destroy(c);
     return rc;
   };
+  // (experiment: CMPC_SPIN_WAIT=1 asks the runtime to spin instead of block
+  // in its waits; it takes effect only before the device's first use)
+  if (const char* e = std::getenv("CMPC_SPIN_WAIT"))
+    if (e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   if (hipSetDevice(device) != hipSuccess) return cleanup(fail("hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail("hipStreamCreate failed"));
