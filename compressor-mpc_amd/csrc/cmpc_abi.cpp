@@ -191,6 +191,8 @@ struct cmpc_ctx {
   int last_solve = 0;                   // kernel launched by the last solve
   int step_variant = CMPC_STEP_AUTO;    // cmpc_set_step_variant
   int cus = 0;                          // compute units of the device (0: not yet queried)
+  bool lds_layout_ok = false;           // lds_layout holds build_lds_layout(d, L)
+  BuildParams lds_layout{};             // (a function of the dimensions only)
   int last_step_fused = 0;
   // timing
   int timing = 0;  // bit k: kernel k (CMPC_KERNEL_*) is timed
@@ -1491,7 +1493,26 @@ static int build_params(cmpc_ctx* c, BuildParams& P) {
     }
   }
   P.dmax = dmax;
-  build_lds_layout(d, L, &P);
+  // the LDS layout and the device's CU count are fixed per context: computed
+  // once (the layout search and the attribute query are host time on every
+  // launch of a small batch, whose kernels take tens of microseconds)
+  if (!c->lds_layout_ok) {
+    build_lds_layout(d, L, &c->lds_layout);
+    c->lds_layout_ok = true;
+  }
+  {
+    const BuildParams& T = c->lds_layout;
+    P.lds_block = T.lds_block;
+    P.yl_stride = T.yl_stride;
+    P.lds_per_wave = T.lds_per_wave;
+    std::memcpy(P.line_off, T.line_off, sizeof P.line_off);
+    P.line_rs = T.line_rs;
+    P.w_off = T.w_off;
+    P.zs_off = T.zs_off;
+    P.zl_stride = T.zl_stride;
+    P.nbound = T.nbound;
+    std::memcpy(P.bound, T.bound, sizeof P.bound);
+  }
   if (L.rec_len > 2 * 64 * CMPC_REC_CHUNKS) return fail("lin record too long for the build kernel");
   const size_t lds_bytes = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
   if (lds_bytes > 160 * 1024) return fail("horizon/delays too long for the build kernel's LDS");
@@ -1499,9 +1520,8 @@ static int build_params(cmpc_ctx* c, BuildParams& P) {
     // persistent grid: the launcher caps this at (resident workgroups per CU,
     // from the occupancy query: registers and LDS) x CUs, so no workgroup
     // waits for a second round
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    P.cus = cus;
+    if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    P.cus = c->cus > 0 ? c->cus : 256;
     P.grid = std::max(1, (c->nqp + CMPC_BUILD_WAVES - 1) / CMPC_BUILD_WAVES);
   }
   cmpc_rows_layout(d, L.nd, L.nobs, L.rec_len, &P.rows);  // cached per dimension set

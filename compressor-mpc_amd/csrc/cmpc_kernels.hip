@@ -641,8 +641,11 @@ void cmpc_build_kernel(BuildParams P) {
 #endif
 }
 
+#ifndef CMPC_SOLVE_WPE_SMALL
+#define CMPC_SOLVE_WPE_SMALL 2  // waves per SIMD of the nV < 6 iterate kernel
+#endif
 #ifndef CMPC_SOLVE_WPE
-#define CMPC_SOLVE_WPE(N) ((N) >= 6 ? 1 : 2)
+#define CMPC_SOLVE_WPE(N) ((N) >= 6 ? 1 : CMPC_SOLVE_WPE_SMALL)
 #endif
 
 // H^-1 of one lane as column `base` of a [N*N][T] lane-contiguous LDS array

@@ -96,6 +96,19 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
 #pragma unroll
             for (int c = 0; c < NU; ++c)
               dother[mv * (SM1 * NU) + rk * NU + c] = P.du_other[(size_t)q * NVO + rk * N + mv * NU + c];
+      } else if (SM1 == 1 && !(base_lane & 1)) {
+        // two sub-controllers on lanes (2i, 2i + 1), as every caller places
+        // a scenario's pair: the other plan is the partner lane's, a
+        // quad_perm [1,0,3,2] DPP move instead of an LDS permute
+#pragma unroll
+        for (int mv = 0; mv < M; ++mv)
+#pragma unroll
+          for (int c = 0; c < NU; ++c) {
+            const double v = dprev[mv * NU + c];
+            const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, true);
+            const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, true);
+            dother[mv * NU + c] = __hiloint2double(hi, lo);
+          }
       } else {
 #pragma unroll
         for (int rk = 0; rk < SM1; ++rk) {

@@ -1,7 +1,7 @@
 """A short, repeatable launch sequence of one small-batch kernel for rocprofv3
 --pmc passes: CONFIG (tools/time_small.py names), WHAT = iterate-lane |
 iterate-rows | build | step, N launches after a warm-up.
-usage: python tools/pmc_small.py CONFIG WHAT [N]"""
+usage: python tools/pmc_small.py CONFIG WHAT [N [K]]"""
 import os
 import sys
 
@@ -16,6 +16,8 @@ from time_small import CONFIGS  # noqa: E402
 name, what = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 plant, ctype, p, B, K = CONFIGS[name]
+if len(sys.argv) > 4:
+    K = int(sys.argv[4])
 cfg = cmpc.reference_config(plant, ctype, p=p)
 arr = cmpc.controller_arrays(cfg, reference_setup(plant, ctype))
 lin, u, du, ws = synthetic_batch(cfg, B, seed=11, n_distinct=min(B, 2048))
