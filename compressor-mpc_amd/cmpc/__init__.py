@@ -234,6 +234,12 @@ class Context:
         check(self.lib.cmpc_observe_step(self._h, ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(y_ptr)),
               "cmpc_observe_step")
 
+    def control_step(self, u_full_ptr: int, y_ptr: int, K: int):
+        """NerveCenter::GetNextInput on the device (cmpc_control_step): observe_step,
+        step(K, 0) and observe_apply, one kernel launch where the batch allows."""
+        check(self.lib.cmpc_control_step(self._h, ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(y_ptr), K),
+              "cmpc_control_step")
+
     def observe_apply(self):
         """UpdateU: ObserveAPriori with the own first move, then u_old += du."""
         check(self.lib.cmpc_observe_apply(self._h), "cmpc_observe_apply")

@@ -801,10 +801,11 @@ int cmpc_set_observer(cmpc_ctx* c, int s, int n_outputs, const double* M) {
 
 int cmpc_observer_len(const cmpc_ctx* c) { return c ? c->obs_len : 0; }
 
-// linearise every QP slot at its own x_hat (observer state) and store C;
-// with_post: the a-posteriori update of each slot first, in the same kernel
-static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y, bool with_post) {
-  ProduceParams P;
+// the producer's per-QP parameters: every QP slot linearised at its own
+// x_hat (observer state), C stored; with_post: the a-posteriori update of
+// each slot first, in the same kernel
+static int observer_produce_params(cmpc_ctx* c, const double* u_full, const double* y, bool with_post,
+                                   ProduceParams& P) {
   int no = 0;
   int io[CMPC_MAX_S_PRODUCE * CMPC_MAX_INPUTS], oi[CMPC_MAX_S_PRODUCE * 4];
   for (int s = 0; s < c->d.S; ++s) {
@@ -837,6 +838,12 @@ static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y, 
     P.obs = c->obs;
     P.obs_ntot = c->L.ntot;
   }
+  return 0;
+}
+
+static int observer_produce(cmpc_ctx* c, const double* u_full, const double* y, bool with_post) {
+  ProduceParams P;
+  if (observer_produce_params(c, u_full, y, with_post, P)) return -1;
   c->lin_bound = nullptr;
   TimedLaunch tl(c, CMPC_KERNEL_PRODUCE);
   if (tl.begin()) return -1;
@@ -905,6 +912,53 @@ int cmpc_observe_apply(cmpc_ctx* c) {
   return tl.end();
 }
 
+static int build_params(cmpc_ctx* c, BuildParams& P);
+
+// NerveCenter::GetNextInput on the device: cmpc_observe_step + cmpc_step(K,
+// 0) + cmpc_observe_apply, as one kernel where the batch takes the
+// one-QP-per-wave fused step (cmpc_control_step_kernel), else the three calls.
+int cmpc_control_step(cmpc_ctx* c, const double* u_full, const double* y, int K) {
+  if (!c) return fail("null context");
+  if (!u_full || !y) return fail("cmpc_control_step: null argument");
+  if (K < 0) return fail("K must be >= 0");
+  if (c->obs_plant < 0) return fail("cmpc_control_step: call cmpc_observer_init first");
+  HIP_TRY(hipSetDevice(c->device));
+  if (observer_upload_M(c)) return -1;
+  if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const cmpc_dims& d = c->d;
+  const bool fuse = K > 0 && c->step_variant != CMPC_STEP_SPLIT && c->build_variant == CMPC_BUILD_AUTO &&
+                    c->solve_variant == CMPC_SOLVE_AUTO && (c->nqp + 3) / 4 < 4 * std::max(c->cus, 1) &&
+                    c->L.nuo == (d.S - 1) * d.nu;
+  if (fuse) {
+    if (ensure_cfg(c)) return -1;
+    ControlStepParams C;
+    std::memset(&C, 0, sizeof C);
+    if (observer_produce_params(c, u_full, y, true, C.pr)) return -1;
+    c->lin_bound = nullptr;  // the build reads the produced records
+    if (build_params(c, C.b)) return -1;
+    solve_params(c, &C.b.sv);
+    C.b.sv.K = K;
+    C.b.sv.flags = 0;  // u_old += du is the a-priori phase's
+    observer_params(c, &C.ob);
+    C.pr_off = ((C.pr.S * C.pr.rec_len + C.pr.naug + 3) / 4) * 2;  // doubles, 16-byte aligned
+    TimedLaunch tl(c, CMPC_KERNEL_STEP);
+    if (tl.begin()) return -1;
+    int solver = 0;
+    if (cmpc_launch_control_step(C, d.ns, d.ny, d.nu, d.m, c->stream, &solver) == 0) {
+      if (check_launch("control step kernel")) return -1;
+      c->last_build = CMPC_BUILD_WAVE;
+      c->last_solve = solver;
+      c->last_step_fused = 1;
+      c->obs_steps++;  // the delay-block rings advance by one (cmpc_observe_apply)
+      return tl.end();
+    }
+    cmpc_launch_events = LaunchEvents{};
+  }
+  if (cmpc_observe_step(c, u_full, y)) return -1;
+  if (cmpc_step(c, K, 0)) return -1;
+  return cmpc_observe_apply(c);
+}
+
 // copies host arrays (nullptr entries skipped) into the context's staging
 // buffer on its stream; returns their device addresses
 // host arrays of up to this many doubles are read by the kernels in place
@@ -961,6 +1015,21 @@ int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
   const double* d[2];
   if (stage_host(c, h, n, 2, d)) return -1;
   const int rc = cmpc_observe_step(c, d[0], d[1]);
+  return stage_done(c) ? -1 : rc;
+}
+
+int cmpc_control_step_host(cmpc_ctx* c, const double* u_full, const double* y, int K) {
+  if (!c) return fail("null context");
+  if (c->obs_plant < 0) return fail("cmpc_control_step_host: call cmpc_observer_init first");
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(c->obs_plant, &ns, &ni, &no, &nci)) return fail("unknown plant");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t B = c->d.B;
+  const double* h[2] = {u_full, y};
+  const size_t n[2] = {B * ni, B * no};
+  const double* d[2];
+  if (stage_host(c, h, n, 2, d)) return -1;
+  const int rc = cmpc_control_step(c, d[0], d[1], K);
   return stage_done(c) ? -1 : rc;
 }
 

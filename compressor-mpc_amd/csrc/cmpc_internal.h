@@ -215,6 +215,19 @@ struct ObserverParams {
   int rot[CMPC_MAX_INPUTS];     // ring position of block k's first state (step count mod D - 1)
 };
 
+// One-launch control step (cmpc_control_step, cmpc_kernels.hip): the
+// producer (per-QP mode with the a-posteriori update), the fused build + K
+// iterations and the observer's a-priori update of a small batch.  pr_off:
+// the producer rows' LDS offset (doubles) after its element table.
+struct ControlStepParams {
+  BuildParams b;
+  ProduceParams pr;
+  ObserverParams ob;
+  int pr_off;
+};
+int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu, int m, void* stream,
+                             int* solver);
+
 // One Jacobi iteration of the sub-controller-sharded cooperative loop
 // (coupled.hip).
 struct CoupledParams {

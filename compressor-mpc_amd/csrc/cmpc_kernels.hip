@@ -28,6 +28,8 @@
 
 #include "cmpc_internal.h"
 #include "dpp_blocks.inc"
+#include "observer_body.h"
+#include "produce_body.h"
 #include "solve_rows.h"
 #include "lane_solve.h"
 
@@ -138,10 +140,8 @@
 // (lane_solve.h; a scenario's sub-controllers are adjacent waves, so adjacent
 // lanes).  Even FUSE values record the working-set trace.  The QP is stored
 // either way (cmpc_download_qp).
-template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE = 0>
-__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES)
-__attribute__((amdgpu_waves_per_eu(FUSE ? 1 : 4, FUSE ? 1 : 4)))
-void cmpc_build_kernel(BuildParams P) {
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE>
+__device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
   constexpr int NG = M * NUT + 1;  // gather lanes per row: QP columns (move k, input c), then z
@@ -639,6 +639,81 @@ void cmpc_build_kernel(BuildParams P) {
     dbg[14] = (double)(blockIdx.x * CMPC_BUILD_WAVES + wave);
   }
 #endif
+}
+
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE = 0>
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES)
+__attribute__((amdgpu_waves_per_eu(FUSE ? 1 : 4, FUSE ? 1 : 4)))
+void cmpc_build_kernel(BuildParams P) {
+  build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(P);
+}
+
+// ---------------------------------------------------------------------------
+// One-launch control step (cmpc_control_step): NerveCenter::GetNextInput for
+// a small batch on the device in one kernel, the workgroup's four QP slots
+// (one per wave):
+//   1. ObserveAPosteriori + Update (linearise, discretise, the lin record):
+//      the producer body (produce_body.h), wave 0, one slot per DPP row;
+//   2. GenerateInitialQP + the K Jacobi iterations: the fused build + solve
+//      (build_wave_body, FUSE 1: row solver of each wave; FUSE 3: the lane
+//      solver of wave 0);
+//   3. UpdateU (ObserveAPriori, u_old += du): observer_body.h, wave 0.
+// Workgroup barriers between the phases order the global stores of one
+// phase before the next phase's loads (one CU, write-through L0).  The
+// producer's table and rows overlay the build's dynamic LDS before the build
+// starts.
+// ---------------------------------------------------------------------------
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE>
+__global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void cmpc_control_step_kernel(ControlStepParams C) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int PLANT = NS == 11 ? CMPC_PLANT_PARALLEL : CMPC_PLANT_SERIAL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int* src = reinterpret_cast<int*>(smem);
+  int* dmap = src + C.pr.S * C.pr.rec_len;
+  cmpc_prod::produce_table<PLANT>(C.pr, src, dmap, threadIdx.x, 64 * CMPC_BUILD_WAVES);
+  __syncthreads();
+  if (wave == 0)
+    cmpc_prod::produce_row<PLANT>(C.pr, smem + C.pr_off + (lane >> 4) * cmpc_prod::kScnLds, src, dmap,
+                                  blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+  __syncthreads();
+  build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(C.b);
+  __syncthreads();
+  if (wave == 0) obs_prior_row<NS, NUT>(C.ob, blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+}
+
+#define CONTROL_CASE(NS_, NY_, NU_, M_, FUSE_)                                              \
+  if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {        \
+    auto k_ = cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_>;                      \
+    if (lds > 64 * 1024)                                                                      \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+    *solver = FUSE_ == 1 ? CMPC_SOLVE_ROWS : CMPC_SOLVE_LANE;                                 \
+    cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, C);      \
+    return 0;                                                                                 \
+  }
+
+int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu, int m, void* stream,
+                             int* solver) {
+  hipStream_t s = (hipStream_t)stream;
+  const BuildParams& P = C.b;
+  if (P.grid * CMPC_BUILD_WAVES < P.nqp || P.sv.trace) return -1;
+  if (C.pr.S != P.S || !C.pr.per_qp || !C.pr.obs_M) return -1;
+  size_t lds = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
+  lds = std::max(lds, sizeof(double) * ((size_t)C.pr_off + 4 * cmpc_prod::kScnLds));
+  if (lds > 160 * 1024) return -1;
+  if (P.S == 1) {
+    if (P.lds_per_wave < ny * (m * 4 + 1) * (nu * m) + 4 * (nu * m) * (nu * m)) return -1;
+    CONTROL_CASE(11, 3, 4, 2, 1)  // parallel centralized
+    CONTROL_CASE(10, 4, 4, 2, 1)  // serial centralized
+    return -1;
+  }
+  if (CMPC_BUILD_WAVES % P.S) return -1;
+  CONTROL_CASE(11, 3, 2, 2, 3)  // parallel coop
+  CONTROL_CASE(11, 2, 2, 2, 3)  // parallel ncoop
+  CONTROL_CASE(10, 2, 2, 2, 3)  // serial ncoop
+  CONTROL_CASE(10, 4, 2, 2, 3)  // serial coop
+  return -1;
 }
 
 #ifndef CMPC_SOLVE_WPE_SMALL

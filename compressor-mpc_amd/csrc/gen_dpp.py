@@ -168,7 +168,7 @@ def gacc(nut, nu, mm):
 
 
 def main():
-    parts = ["// Generated by gen_dpp.py — do not edit.\n",
+    parts = ["// Generated by gen_dpp.py — do not edit.\n#pragma once\n",
              "template <int NS> __device__ __forceinline__ void prop_dpp(double, const double*,"
              " double&, double&);\n",
              "template <int LB, int NU, int M> __device__ __forceinline__ void accum_dpp("

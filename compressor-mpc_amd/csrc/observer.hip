@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "cmpc_internal.h"
+#include "observer_body.h"
 
 namespace {
 
@@ -67,86 +68,8 @@ __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_init_kernel(ObserverPara
 // the logical order.  Every source value is loaded before any store.
 template <int NS, int NUT>
 __global__ __launch_bounds__(64 * kWaves) void cmpc_obs_prior_kernel(ObserverParams P) {
-  static_assert(NS <= 16 && NUT <= 16, "a QP's 16-lane row holds a state row per lane and every input");
-  const int lane = threadIdx.x & 15, base = threadIdx.x & 48;
-  const int nobs = P.nobs, nd = P.nd;
-  // delay tables in registers (compile-time indices: a runtime-indexed
-  // kernel-argument read is a dependent memory load)
-  int dl[NUT], din[NUT], blk[NUT], rot[NUT];
-#pragma unroll
-  for (int i = 0; i < NUT; ++i) {
-    dl[i] = P.delay[i];
-    din[i] = P.dinput[i];
-    blk[i] = P.blk[i];
-    rot[i] = P.rot[i];
-  }
-  auto pick = [](const int* a, int k) {
-    int v = a[0];
-#pragma unroll
-    for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
-    return v;
-  };
-  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4 + (base >> 4);
-  const bool valid = q_raw < P.nqp;  // (an idle row keeps the wave's shuffles)
-  const int q = valid ? q_raw : P.nqp - 1;
-  double* st = P.obs + (size_t)q * P.obs_len;
-  double* dx = st + NS;
-  const double* rec = P.lin + (size_t)q * P.rec_len;
-  double* uo = P.u_old + (size_t)q * NUT;
-  // lanes < nu_tot: u_old, du = own first move (others zero, nerve_center.h:323-328),
-  // or the caller's full input change (DistributedController::UpdateU(du))
-  const int li = lane < NUT ? lane : 0;
-  const double u0 = uo[li];
-  const double du = P.du_full ? ((lane < NUT) ? P.du_full[(size_t)q * NUT + lane] : 0.0)
-                              : ((lane < P.nu) ? P.du_old[(size_t)q * P.nV + lane] : 0.0);
-  // lanes < nd: delayed-input slot, the block's first state (ring head), the
-  // input's u_old
-  const int lk = lane < nd ? lane : 0;
-  const int ik = pick(din, lk);
-  const int head = pick(blk, lk) + pick(rot, lk);
-  const double slot = dx[nobs + lk];
-  const double first = dx[head];
-  const double useg = uo[ik];
-  // lanes < ns: row of B (sub-controller input order) and f
-  const int ls = lane < NS ? lane : 0;
-  double brow[NUT];
-#pragma unroll
-  for (int i = 0; i < NUT; ++i) brow[i] = rec[P.off_B + ls * NUT + i];
-  const double fl = rec[P.off_f + ls];
-  // du' = du + u_old on delayed inputs (AdjustAppliedInput); dx' slots minus
-  // u_old (AdjustFirstDelayedStates)
-  const double dup = pick(dl, li) ? du + u0 : du;
-  const double seg = slot - useg;
-  double dupv[NUT];
-#pragma unroll
-  for (int i = 0; i < NUT; ++i) dupv[i] = __shfl(dup, base + i, 64);
-  // states: (B du')[:ns] + (Adelay seg) + f
-  double bsum = 0.0;
-#pragma unroll
-  for (int i = 0; i < NUT; ++i)
-    if (!dl[i]) bsum += brow[i] * dupv[i];
-  double tsum = 0.0;
-#pragma unroll
-  for (int k = 0; k < NUT; ++k) {
-    const double sk = __shfl(seg, base + k, 64);
-    double bk = brow[0];
-#pragma unroll
-    for (int i = 1; i < NUT; ++i) bk = (din[k] == i) ? brow[i] : bk;
-    if (k < nd) tsum += bk * sk;
-  }
-  const double xn = (bsum + tsum) + fl;
-  double last = dupv[0];  // du' of the block's input: its new last state
-#pragma unroll
-  for (int i = 1; i < NUT; ++i) last = (ik == i) ? dupv[i] : last;
-  WAVE_SYNC();  // all loads above have completed before the first store
-  if (!valid) return;
-  if (lane < NS) dx[lane] = xn;
-  if (lane < nd) {
-    dx[nobs + lane] = first;  // slot k <- first state of block k
-    dx[head] = last;          // the ring advances: this entry becomes the last state
-  }
-  // UpdateU: u_old += du (cmpc_observe_apply: own inputs, the others add zero)
-  if (lane < NUT) uo[lane] = u0 + du;
+  const int q_raw = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4 + ((threadIdx.x & 48) >> 4);
+  obs_prior_row<NS, NUT>(P, q_raw, threadIdx.x & 63);
 }
 
 }  // namespace

@@ -36,6 +36,9 @@
  *                          include/nerve_center.h:313-328)
  *   cmpc_step              cmpc_build + cmpc_iterate = NerveCenter::GetNextInputWithTiming
  *                          include/nerve_center.h:134-182
+ *   cmpc_control_step      the same with the observer (ObserveAPosteriori, Update,
+ *                          UpdateU: libs/observer.cc:8-44, libs/distributed_controller.cc:72-108,
+ *                          include/distributed_controller.h:145-152) = GetNextInput
  *
  * The QP solver is this library's own warm-started dual active-set method
  * (qpOASES 3.2.0 SQProblem::hotstart is not vendored in the reference); it
@@ -358,6 +361,16 @@ int cmpc_observer_init_host(cmpc_ctx* ctx, int plant, double p_in, double p_out,
                             const double* x_init, const double* u_full, const double* y_init,
                             const double* dx_init);
 int cmpc_observe_step_host(cmpc_ctx* ctx, const double* u_full, const double* y);
+/* NerveCenter::GetNextInput (include/nerve_center.h:134-182) on the device:
+ * cmpc_observe_step(u_full, y) + cmpc_step(K, 0) + cmpc_observe_apply() with
+ * the same results bit for bit, as ONE kernel launch for batches the
+ * one-QP-per-wave fused step runs (under one row group per SIMD, AUTO
+ * variants, no trace): observer a posteriori + linearisation, the QP build,
+ * K Jacobi iterations and the a-priori update in one workgroup per four QP
+ * slots.  Elsewhere the three calls.  Plans, statuses and nWSR through
+ * cmpc_download; u_old has moved by the own first moves. */
+int cmpc_control_step(cmpc_ctx* ctx, const double* u_full, const double* y, int K);
+int cmpc_control_step_host(cmpc_ctx* ctx, const double* u_full, const double* y, int K);
 /* Host copies of the observer state rows (B*S x cmpc_observer_len()). */
 int cmpc_get_observer_state(cmpc_ctx* ctx, double* host);
 int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);

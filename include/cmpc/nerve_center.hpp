@@ -796,6 +796,13 @@ class NerveCenter : public ControllerInterface {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<double> u_full(u_offset_);
     for (int c = 0; c < spec_.nu_tot; ++c) u_full[spec_.plant_input_index[c]] += u_old_[c];
+    if (K_ > 0 && (n_timing_iterations < 0 || n_timing_iterations >= K_)) {
+      // the whole step (a posteriori + Update, build, K iterations, UpdateU)
+      // as one launch where the batch allows (cmpc_control_step)
+      Check(cmpc_control_step_host(ctx_, u_full.data(), y, K_), "cmpc_control_step_host");
+      Download();
+      return Finish(0, t0, time_out_ns);
+    }
     // ObserveAPosteriori + Update at each sub-controller's estimate
     Check(cmpc_observe_step_host(ctx_, u_full.data(), y), "cmpc_observe_step_host");
     const int64_t stopped = Step(n_timing_iterations, 0u);

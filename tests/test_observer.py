@@ -357,6 +357,57 @@ def test_gpu_closed_loop_observer_matches_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("plant,ctype,p,B,K", [
+    ("par", "coop", 50, 1, 9),     # B = 1, the reference's own call pattern
+    ("par", "coop", 20, 13, 9),    # a partial last workgroup
+    ("par", "ncoop", 50, 3, 9),
+    ("par", "cent", 20, 5, 3),     # row solver of each wave
+    ("ser", "cent", 100, 1, 1),    # SURVEY config 1 at B = 1
+    ("ser", "coop", 50, 2, 9)])
+def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):
+    """cmpc_control_step (NerveCenter::GetNextInput as one kernel: a
+    posteriori + linearisation, build, K Jacobi iterations, a priori) against
+    cmpc_observe_step + cmpc_step(K, 0) + cmpc_observe_apply on the same
+    state over four steps: plans, statuses, nWSR, records, QPs, observer rows
+    and controller state bit for bit, and the one launch did run."""
+    # operating points near the equilibrium and a small gain (as the closed-loop
+    # test above): the estimate stays where the linearisation is finite
+    cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, p, B, 17, xs=1e-4, us=1e-3, ms=0.01)
+    nq = B * cfg.S
+    ys = [y * (1 + 3e-4 * rng.normal(size=y.shape)) for _ in range(4)]
+    out = []
+    for one in (False, True):
+        with cmpc.Context(cfg, B, device=0) as ctx:
+            ctx.configure(arr)
+            ctx.set_state(np.zeros((nq, cfg.nu_tot)), np.zeros((nq, cfg.nV)), np.zeros(nq, np.uint32))
+            for s_ in range(cfg.S):
+                ctx.set_observer(s_, M[s_])
+            tx, tu = dev(x), dev(u)
+            tys = [dev(a) for a in ys]
+            ctx.observer_init(tx.data_ptr(), tu.data_ptr(), dev(y).data_ptr())
+            ctx.build()
+            ctx.init_warmstart()
+            res = []
+            for t in range(4):
+                if one:
+                    ctx.control_step(tu.data_ptr(), tys[t].data_ptr(), K)
+                    assert ctx.last_step_fused() == 1
+                else:
+                    ctx.observe_step(tu.data_ptr(), tys[t].data_ptr())
+                    ctx.step(K, 0)
+                    ctx.observe_apply()
+                res.append((*ctx.download(), ctx.download_lin(), *ctx.download_qp(), ctx.observer_state(),
+                            *ctx.get_state()))
+            out.append(res)
+    for t, (a, b) in enumerate(zip(*out)):
+        for i, (va, vb) in enumerate(zip(a, b)):
+            if va is None:
+                continue
+            assert np.array_equal(va, vb, equal_nan=True), (t, i)
+    assert np.isfinite(out[1][-1][3]).all() and (out[1][-1][1] == 0).mean() > 0.5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", GC.NAMES)
 def test_gpu_step0_golden_through_observer(name):
     """Initialize + GenerateInitialQP through the observer path reproduce the
