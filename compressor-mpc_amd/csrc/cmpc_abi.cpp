@@ -191,6 +191,7 @@ struct cmpc_ctx {
   int last_solve = 0;                   // kernel launched by the last solve
   int step_variant = CMPC_STEP_AUTO;    // cmpc_set_step_variant
   int cus = 0;                          // compute units of the device (0: not yet queried)
+  std::vector<const void*> bound_ok;    // device pointers cmpc_bind_* validated before
   bool lds_layout_ok = false;           // lds_layout holds build_lds_layout(d, L)
   BuildParams lds_layout{};             // (a function of the dimensions only)
   int last_step_fused = 0;
@@ -611,12 +612,25 @@ int cmpc_download_lin(cmpc_ctx* c, double* lin) {
 
 void* cmpc_lin_device(cmpc_ctx* c) { return c ? (void*)c->lin : nullptr; }
 
+// p is device memory of the context's device.  A rotation over a few bound
+// buffers (the bench binds four per step) queries each once: the runtime's
+// pointer lookup is several microseconds of host time per call, more than a
+// small batch's kernels take
+static bool device_ptr_ok(cmpc_ctx* c, const void* p) {
+  for (const void* v : c->bound_ok)
+    if (v == p) return true;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice || a.device != c->device)
+    return false;
+  if (c->bound_ok.size() >= 64) c->bound_ok.erase(c->bound_ok.begin());
+  c->bound_ok.push_back(p);
+  return true;
+}
+
 int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
   if (!c) return fail("null context");
   if (lin_device) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, lin_device) != hipSuccess || a.type != hipMemoryTypeDevice ||
-        a.device != c->device)
+    if (!device_ptr_ok(c, lin_device))
       return fail("cmpc_bind_lin: not a device pointer on the context's device");
     // the build kernels read records with 16-byte loads (LDS-DMA / double2)
     if (reinterpret_cast<uintptr_t>(lin_device) % 16 != 0)
@@ -637,12 +651,8 @@ int cmpc_bind_state(cmpc_ctx* c, double* u_old, double* du_old, uint32_t* ws) {
   }
   if (nnull != 0) return fail("cmpc_bind_state: bind all three state arrays or none");
   const void* ptrs[] = {u_old, du_old, ws};
-  for (const void* p : ptrs) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice ||
-        a.device != c->device)
-      return fail("cmpc_bind_state: not a device pointer on the context's device");
-  }
+  for (const void* p : ptrs)
+    if (!device_ptr_ok(c, p)) return fail("cmpc_bind_state: not a device pointer on the context's device");
   if (reinterpret_cast<uintptr_t>(u_old) % 8 || reinterpret_cast<uintptr_t>(du_old) % 8 ||
       reinterpret_cast<uintptr_t>(ws) % 4)
     return fail("cmpc_bind_state: misaligned state array");
