@@ -240,6 +240,17 @@ class Context:
         check(self.lib.cmpc_control_step(self._h, ctypes.c_void_p(u_full_ptr), ctypes.c_void_p(y_ptr), K),
               "cmpc_control_step")
 
+    def control_step_download(self, u_full: np.ndarray, y: np.ndarray, K: int):
+        """cmpc_control_step_download: the control step from host arrays and its
+        plans, statuses and nWSR (polled completion for one-workgroup batches)."""
+        du = np.zeros((self.nqp, self.layout.nV))
+        status = np.zeros(self.nqp, np.int32)
+        nwsr = np.zeros(self.nqp, np.int32)
+        check(self.lib.cmpc_control_step_download(self._h, dptr(np.ascontiguousarray(u_full, np.float64)),
+                                                  dptr(np.ascontiguousarray(y, np.float64)), K, dptr(du),
+                                                  iptr(status), iptr(nwsr)), "cmpc_control_step_download")
+        return du, status, nwsr
+
     def observe_apply(self):
         """UpdateU: ObserveAPriori with the own first move, then u_old += du."""
         check(self.lib.cmpc_observe_apply(self._h), "cmpc_observe_apply")

@@ -102,7 +102,7 @@ EXPORTS = (
     "cmpc_get_input", "cmpc_get_input_host", "cmpc_update_u", "cmpc_update_u_host",
     "cmpc_set_observer", "cmpc_observer_len", "cmpc_observer_init", "cmpc_observe_step",
     "cmpc_observe_apply", "cmpc_get_observer_state", "cmpc_set_observer_state",
-    "cmpc_observer_init_host", "cmpc_observe_step_host", "cmpc_control_step", "cmpc_control_step_host",
+    "cmpc_observer_init_host", "cmpc_observe_step_host", "cmpc_control_step", "cmpc_control_step_host", "cmpc_control_step_download",
     "cmpc_sim_create", "cmpc_sim_destroy", "cmpc_sim_set_stream", "cmpc_sim_reset",
     "cmpc_sim_set_input", "cmpc_sim_set_offset", "cmpc_sim_restart", "cmpc_sim_plant_input_offset",
     "cmpc_sim_plant_input", "cmpc_sim_integrate", "cmpc_sim_output",
@@ -186,6 +186,8 @@ def load_library(path: str = LIB_PATH):
         "cmpc_observe_apply": ([c_void], ctypes.c_int),
         "cmpc_control_step": ([c_void, c_void, c_void, ctypes.c_int], ctypes.c_int),
         "cmpc_control_step_host": ([c_void, P(dbl), P(dbl), ctypes.c_int], ctypes.c_int),
+        "cmpc_control_step_download": ([c_void, P(dbl), P(dbl), ctypes.c_int, P(dbl), P(i32), P(i32)],
+                                       ctypes.c_int),
         "cmpc_observer_init_host": ([c_void, ctypes.c_int, dbl, dbl, dbl, P(i32), P(i32), P(dbl),
                                      P(dbl), P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_observe_step_host": ([c_void, P(dbl), P(dbl)], ctypes.c_int),

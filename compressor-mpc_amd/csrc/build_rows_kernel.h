@@ -700,8 +700,7 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   const size_t lds = sizeof(double) * ((size_t)P.rows.lds_block + (size_t)P.rows.per_wave * WPG);
   if (lds > 160 * 1024) return -1;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cmpc_allow_lds(reinterpret_cast<const void*>(kern), lds);
   int per_cu = cmpc_blocks_per_cu(kern, 64 * WPG, lds);
   if (per_cu < 1) per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   per_cu = std::min(per_cu, std::max(1, 4 * WPE / WPG));  // the register budget's waves per SIMD

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "cmpc_internal.h"
@@ -167,6 +168,9 @@ struct cmpc_ctx {
   int32_t *status = nullptr, *nwsr = nullptr, *ntrace = nullptr;
   char* out_block = nullptr;  // du | status | nwsr in one allocation: one D2H for cmpc_download
   bool out_host = false;      // out_block is page-locked host memory the kernels write in place
+  uint32_t* done_host = nullptr;  // out_host: the control step's completion word (after the block)
+  uint32_t* done_dev = nullptr;   // its device address
+  uint32_t done_seq = 0;
   size_t out_st = 0, out_nw = 0, out_len = 0;  // byte offsets of status, nwsr; block length
   uint8_t* trace = nullptr;
   size_t trace_cap = 0;
@@ -452,12 +456,15 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
     char* dev_out = nullptr;
     if (n <= CMPC_HOST_OUT_MAX_QP) {
       void* dv = nullptr;
-      if (hipHostMalloc(reinterpret_cast<void**>(&c->out_block), c->out_len, hipHostMallocCoherent) != hipSuccess ||
+      const size_t done_off = up16(c->out_len);
+      if (hipHostMalloc(reinterpret_cast<void**>(&c->out_block), done_off + 16, hipHostMallocCoherent) != hipSuccess ||
           hipHostGetDevicePointer(&dv, c->out_block, 0) != hipSuccess)
         return cleanup(fail("hipHostMalloc failed"));
       c->out_host = true;
-      std::memset(c->out_block, 0, c->out_len);
+      std::memset(c->out_block, 0, done_off + 16);
       dev_out = reinterpret_cast<char*>(dv);
+      c->done_host = reinterpret_cast<uint32_t*>(c->out_block + done_off);
+      c->done_dev = reinterpret_cast<uint32_t*>(dev_out + done_off);
     } else {
       if (hipMalloc(&c->out_block, c->out_len) != hipSuccess)
         return cleanup(fail("hipMalloc failed (batch too large for device memory?)"));
@@ -927,7 +934,16 @@ static int build_params(cmpc_ctx* c, BuildParams& P);
 // NerveCenter::GetNextInput on the device: cmpc_observe_step + cmpc_step(K,
 // 0) + cmpc_observe_apply, as one kernel where the batch takes the
 // one-QP-per-wave fused step (cmpc_control_step_kernel), else the three calls.
+static int control_step(cmpc_ctx* c, const double* u_full, const double* y, int K, bool* flagged);
+
 int cmpc_control_step(cmpc_ctx* c, const double* u_full, const double* y, int K) {
+  return control_step(c, u_full, y, K, nullptr);
+}
+
+// flagged (optional): set when the launch stores c->done_seq into
+// c->done_host once its results are in place
+static int control_step(cmpc_ctx* c, const double* u_full, const double* y, int K, bool* flagged) {
+  if (flagged) *flagged = false;
   if (!c) return fail("null context");
   if (!u_full || !y) return fail("cmpc_control_step: null argument");
   if (K < 0) return fail("K must be >= 0");
@@ -951,6 +967,9 @@ int cmpc_control_step(cmpc_ctx* c, const double* u_full, const double* y, int K)
     C.b.sv.flags = 0;  // u_old += du is the a-priori phase's
     observer_params(c, &C.ob);
     C.pr_off = ((C.pr.S * C.pr.rec_len + C.pr.naug + 3) / 4) * 2;  // doubles, 16-byte aligned
+    const bool flag = flagged && c->done_dev && C.b.grid == 1;
+    C.done = flag ? c->done_dev : nullptr;
+    C.seq = flag ? ++c->done_seq : 0u;
     TimedLaunch tl(c, CMPC_KERNEL_STEP);
     if (tl.begin()) return -1;
     int solver = 0;
@@ -960,6 +979,7 @@ int cmpc_control_step(cmpc_ctx* c, const double* u_full, const double* y, int K)
       c->last_solve = solver;
       c->last_step_fused = 1;
       c->obs_steps++;  // the delay-block rings advance by one (cmpc_observe_apply)
+      if (flagged) *flagged = flag;
       return tl.end();
     }
     cmpc_launch_events = LaunchEvents{};
@@ -1026,6 +1046,41 @@ int cmpc_observe_step_host(cmpc_ctx* c, const double* u_full, const double* y) {
   if (stage_host(c, h, n, 2, d)) return -1;
   const int rc = cmpc_observe_step(c, d[0], d[1]);
   return stage_done(c) ? -1 : rc;
+}
+
+// cmpc_control_step_host + cmpc_download: a one-workgroup launch signals its
+// completion word, which the host polls (the results are in page-locked host
+// memory already) instead of a stream synchronisation; anything else, and a
+// poll that has not seen the word after a second, synchronises the stream.
+int cmpc_control_step_download(cmpc_ctx* c, const double* u_full, const double* y, int K, double* du,
+                               int32_t* status, int32_t* nwsr) {
+  if (!c) return fail("null context");
+  if (c->obs_plant < 0) return fail("cmpc_control_step_download: call cmpc_observer_init first");
+  int ns = 0, ni = 0, no = 0, nci = 0;
+  if (cmpc_plant_dims(c->obs_plant, &ns, &ni, &no, &nci)) return fail("unknown plant");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t B = c->d.B;
+  const double* h[2] = {u_full, y};
+  const size_t n[2] = {B * ni, B * no};
+  const double* d[2];
+  if (stage_host(c, h, n, 2, d)) return -1;
+  bool flagged = false;
+  const int rc = control_step(c, d[0], d[1], K, &flagged);
+  if (stage_done(c) || rc) return -1;
+  if (!flagged || !c->out_host) return cmpc_download(c, du, status, nwsr);
+  const volatile uint32_t* w = c->done_host;
+  const uint32_t want = c->done_seq;
+  const auto t0 = std::chrono::steady_clock::now();
+  long spins = 0;
+  while (__atomic_load_n(const_cast<const uint32_t*>(w), __ATOMIC_ACQUIRE) != want) {
+    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1))
+      return cmpc_download(c, du, status, nwsr);  // (the stream synchronisation path)
+  }
+  const size_t nq = (size_t)c->nqp;
+  if (du) std::memcpy(du, c->out_block, sizeof(double) * nq * c->L.nV);
+  if (status) std::memcpy(status, c->out_block + c->out_st, sizeof(int32_t) * nq);
+  if (nwsr) std::memcpy(nwsr, c->out_block + c->out_nw, sizeof(int32_t) * nq);
+  return 0;
 }
 
 int cmpc_control_step_host(cmpc_ctx* c, const double* u_full, const double* y, int K) {

@@ -51,6 +51,23 @@ inline int cmpc_blocks_per_cu(F kernel, int threads, size_t lds) {
   return v;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, size):
+// a launcher that set it on every launch paid its host time per step (a
+// config-5 step: 57 us of wall time per 41 us kernel)
+inline void cmpc_allow_lds(const void* kernel, size_t bytes) {
+  struct Entry {
+    const void* k;
+    size_t bytes;
+  };
+  static thread_local Entry cache[32];
+  static thread_local int n = 0;
+  for (int i = 0; i < n && i < 32; ++i)
+    if (cache[i].k == kernel && cache[i].bytes >= bytes) return;
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  cache[n % 32] = Entry{kernel, bytes};
+  ++n;
+}
+
 #define CMPC_ND_MAX 4            // delayed inputs supported by the build kernel
 #define CMPC_BUILD_WAVES 4       // waves per build workgroup (one QP per wave at a time)
 #ifndef CMPC_ROWS_U
@@ -224,6 +241,11 @@ struct ControlStepParams {
   ProduceParams pr;
   ObserverParams ob;
   int pr_off;
+  // one-workgroup launches: after the last phase, seq is stored to *done
+  // (page-locked host memory) with a system-scope release, so the host can
+  // wait for the results by polling instead of a stream synchronisation
+  uint32_t* done;
+  uint32_t seq;
 };
 int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu, int m, void* stream,
                              int* solver);

@@ -679,15 +679,19 @@ void cmpc_control_step_kernel(ControlStepParams C) {
   __syncthreads();
   build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(C.b);
   __syncthreads();
-  if (wave == 0) obs_prior_row<NS, NUT>(C.ob, blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+  if (wave == 0) {
+    obs_prior_row<NS, NUT>(C.ob, blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+    // every wave's results were stored before the barrier above, wave 0's
+    // a-priori stores before this release (a vector store, system scope)
+    if (C.done && lane == 0) __hip_atomic_store(C.done, C.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 #define CONTROL_CASE(NS_, NY_, NU_, M_, FUSE_)                                              \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {        \
     auto k_ = cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_>;                      \
     if (lds > 64 * 1024)                                                                      \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+      cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds);        \
     *solver = FUSE_ == 1 ? CMPC_SOLVE_ROWS : CMPC_SOLVE_LANE;                                 \
     cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, C);      \
     return 0;                                                                                 \
@@ -815,9 +819,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
     const size_t lds = sizeof(double) * ((size_t)P.lds_block +                         \
                                          (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);  \
     if (lds > 64 * 1024)                                                               \
-      (void)hipFuncSetAttribute(                                                       \
-          reinterpret_cast<const void*>(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>),   \
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
+      cmpc_allow_lds(reinterpret_cast<const void*>(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>), lds);                       \
     int per_cu = cmpc_blocks_per_cu(cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2>,        \
                                     64 * CMPC_BUILD_WAVES, lds);                       \
     if (per_cu < 1) per_cu = std::max<int>(1, (int)((160 * 1024) / lds));             \
@@ -838,14 +840,12 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
     if (P.sv.trace) {                                                                    \
       auto k_ = cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 2>;                           \
       if (lds > 64 * 1024)                                                               \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                    \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds); \
       cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P); \
     } else {                                                                             \
       auto k_ = cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 1>;                           \
       if (lds > 64 * 1024)                                                               \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                    \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds); \
       cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P); \
     }                                                                                    \
     return 0;                                                                            \
@@ -860,8 +860,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
     auto k_ = P.sv.trace ? cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 4>                 \
                          : cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 3>;                \
     if (lds > 64 * 1024)                                                                 \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_),                      \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);   \
+      cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds);   \
     *solver = CMPC_SOLVE_LANE;                                                           \
     cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, P);   \
     return 0;                                                                            \

@@ -33,12 +33,18 @@ __device__ __forceinline__ void obs_prior_row(const ObserverParams& P, int q_raw
     blk[i] = P.blk[i];
     rot[i] = P.rot[i];
   }
-  auto pick = [](const int* a, int k) {
-    int v = a[0];
-#pragma unroll
-    for (int i = 1; i < NUT; ++i) v = (k == i) ? a[i] : v;
-    return v;
-  };
+  // (a per-lane choice among uniform values: a select chain; written out on
+  // scalars, since inside the one-launch control step the compiler turned a
+  // chain over a local array into a scratch table)
+#define CMPC_PICK(a, k)                                   \
+  ([&]() {                                                \
+    int v_ = a[0];                                        \
+    _Pragma("unroll") for (int i_ = 1; i_ < NUT; ++i_) {  \
+      const int c_ = a[i_];                               \
+      v_ = ((k) == i_) ? c_ : v_;                         \
+    }                                                     \
+    return v_;                                            \
+  }())
   const bool valid = q_raw < P.nqp;  // (an idle row keeps the wave's shuffles)
   const int q = valid ? q_raw : P.nqp - 1;
   double* st = P.obs + (size_t)q * P.obs_len;
@@ -54,8 +60,8 @@ __device__ __forceinline__ void obs_prior_row(const ObserverParams& P, int q_raw
   // lanes < nd: delayed-input slot, the block's first state (ring head), the
   // input's u_old
   const int lk = lane < nd ? lane : 0;
-  const int ik = pick(din, lk);
-  const int head = pick(blk, lk) + pick(rot, lk);
+  const int ik = CMPC_PICK(P.dinput, lk);
+  const int head = CMPC_PICK(P.blk, lk) + CMPC_PICK(P.rot, lk);
   const double slot = dx[nobs + lk];
   const double first = dx[head];
   const double useg = uo[ik];
@@ -67,7 +73,7 @@ __device__ __forceinline__ void obs_prior_row(const ObserverParams& P, int q_raw
   const double fl = rec[P.off_f + ls];
   // du' = du + u_old on delayed inputs (AdjustAppliedInput); dx' slots minus
   // u_old (AdjustFirstDelayedStates)
-  const double dup = pick(dl, li) ? du + u0 : du;
+  const double dup = CMPC_PICK(P.delay, li) ? du + u0 : du;
   const double seg = slot - useg;
   double dupv[NUT];
 #pragma unroll

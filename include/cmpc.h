@@ -371,6 +371,12 @@ int cmpc_observe_step_host(cmpc_ctx* ctx, const double* u_full, const double* y)
  * cmpc_download; u_old has moved by the own first moves. */
 int cmpc_control_step(cmpc_ctx* ctx, const double* u_full, const double* y, int K);
 int cmpc_control_step_host(cmpc_ctx* ctx, const double* u_full, const double* y, int K);
+/* cmpc_control_step_host + cmpc_download (host arrays in and out; any output
+ * pointer may be NULL), the C++ NerveCenter::GetNextInput path: a one-
+ * workgroup launch (up to four QP slots) marks its completion in page-locked
+ * host memory, which the call polls instead of synchronising the stream. */
+int cmpc_control_step_download(cmpc_ctx* ctx, const double* u_full, const double* y, int K,
+                               double* du, int32_t* status, int32_t* nwsr);
 /* Host copies of the observer state rows (B*S x cmpc_observer_len()). */
 int cmpc_get_observer_state(cmpc_ctx* ctx, double* host);
 int cmpc_set_observer_state(cmpc_ctx* ctx, const double* host);

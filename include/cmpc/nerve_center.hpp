@@ -799,8 +799,11 @@ class NerveCenter : public ControllerInterface {
     if (K_ > 0 && (n_timing_iterations < 0 || n_timing_iterations >= K_)) {
       // the whole step (a posteriori + Update, build, K iterations, UpdateU)
       // as one launch where the batch allows (cmpc_control_step)
-      Check(cmpc_control_step_host(ctx_, u_full.data(), y, K_), "cmpc_control_step_host");
-      Download();
+      du_.resize(static_cast<size_t>(spec_.S()) * spec_.nV());
+      status_.resize(spec_.S());
+      nwsr_.resize(spec_.S());
+      Check(cmpc_control_step_download(ctx_, u_full.data(), y, K_, du_.data(), status_.data(), nwsr_.data()),
+            "cmpc_control_step_download");
       return Finish(0, t0, time_out_ns);
     }
     // ObserveAPosteriori + Update at each sub-controller's estimate

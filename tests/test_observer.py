@@ -376,7 +376,7 @@ def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):
     nq = B * cfg.S
     ys = [y * (1 + 3e-4 * rng.normal(size=y.shape)) for _ in range(4)]
     out = []
-    for one in (False, True):
+    for one in (False, True, "poll"):
         with cmpc.Context(cfg, B, device=0) as ctx:
             ctx.configure(arr)
             ctx.set_state(np.zeros((nq, cfg.nu_tot)), np.zeros((nq, cfg.nV)), np.zeros(nq, np.uint32))
@@ -389,7 +389,11 @@ def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):
             ctx.init_warmstart()
             res = []
             for t in range(4):
-                if one:
+                if one == "poll":  # host arrays in, results back in one call
+                    polled = ctx.control_step_download(u, ys[t], K)
+                    assert ctx.last_step_fused() == 1
+                    assert all(np.array_equal(a, b) for a, b in zip(polled, ctx.download()))
+                elif one:
                     ctx.control_step(tu.data_ptr(), tys[t].data_ptr(), K)
                     assert ctx.last_step_fused() == 1
                 else:
@@ -399,11 +403,12 @@ def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):
                 res.append((*ctx.download(), ctx.download_lin(), *ctx.download_qp(), ctx.observer_state(),
                             *ctx.get_state()))
             out.append(res)
-    for t, (a, b) in enumerate(zip(*out)):
-        for i, (va, vb) in enumerate(zip(a, b)):
-            if va is None:
-                continue
-            assert np.array_equal(va, vb, equal_nan=True), (t, i)
+    for other in out[1:]:
+        for t, (a, b) in enumerate(zip(out[0], other)):
+            for i, (va, vb) in enumerate(zip(a, b)):
+                if va is None:
+                    continue
+                assert np.array_equal(va, vb, equal_nan=True), (t, i)
     assert np.isfinite(out[1][-1][3]).all() and (out[1][-1][1] == 0).mean() > 0.5
 
 
