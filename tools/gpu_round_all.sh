@@ -1,7 +1,7 @@
 #!/bin/bash
 # The round's full GPU record: tools/gpu_round.sh (parity tests, smoke, bench,
 # rocprofv3 stats, PMC passes), the B = 1 adapter latency and trace, the
-# small-batch timings and the config-5 apply-move A/B.  usage: TAG (default ${1:-r4i})
+# small-batch timings and the config-5 apply-move A/B.  usage: TAG (default r4i)
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 bash tools/gpu_round.sh ${1:-r4i} || exit $?
