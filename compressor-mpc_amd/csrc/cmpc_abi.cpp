@@ -1932,7 +1932,11 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
       rc = cmpc_launch_step_wave(P, d.ns, d.ny, d.nu, d.m, c->stream, &solver);
       kind = CMPC_BUILD_WAVE;
     }
-    if (rc) {
+    // AUTO leaves the row kernel's fused step with the lane solver (nV <= 4)
+    // to the two launches, measured faster on every box this round (config 2:
+    // 32.0-32.2 vs 33.7-33.9 us back to back, profiles/r4i_small_batch.txt)
+    const bool rows_lane = c->L.nV <= 4 && c->step_variant == CMPC_STEP_AUTO;
+    if (rc && !(rows_fill && rows_lane)) {
       rc = cmpc_launch_step_rows(P, d.ns, d.ny, d.nu, d.m, c->stream, &solver);
       kind = CMPC_BUILD_ROWS;
     }
