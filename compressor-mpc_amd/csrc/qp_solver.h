@@ -122,9 +122,12 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
   return t;
 }
 
-// Working set: slots 0..K-1 sorted by constraint index j, each with its
-// normal, bound beta and multiplier.  h_a = Hinv * normal_a is recomputed
-// where it is used (registers: the solve kernel runs at 2 waves/SIMD).
+// Working set: slots 0..K-1 in the specification's order (ascending j from
+// the warm start, phase-B additions appended), each with its normal, bound
+// beta and multiplier, and the LDL' factor of M = N' Hinv N with reciprocal
+// pivots R = 1/D (oracle/or_qp.c, spec version 2).  h_a = Hinv * normal_a is
+// recomputed where it is used (registers: the solve kernel runs at 2
+// waves/SIMD).
 // SN (store normals): the explicit normal vectors are kept per slot (N <= 6);
 // for larger N they are rebuilt from (j, side) where they are used
 // (Qp::normal, the same vector bit for bit), which frees 2 N^2 registers per
@@ -138,7 +141,7 @@ struct WSet {
   int j[N], side[N];
   double lam[N];
   double nrm[SN ? N : 1][N], bta[N];
-  double L[N][N], D[N];
+  double L[N][N], D[N], R[N];
 };
 
 // the normal of slot a (stored, or rebuilt from its constraint index)
@@ -152,11 +155,11 @@ CMPC_HD void wset_normal(const Q& q, const WSet<N, SN>& W, int a, double (&n)[N]
   }
 }
 
-// LDL' of the leading K x K block of M (M symmetric); returns false on a
-// non-positive pivot.
+// LDL' of the leading K x K block of M (lower triangle read) with reciprocal
+// pivots R = 1/D (or_qp.c ldl); returns false on a non-positive pivot.
 template <int N>
-CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N],
-                                      double (&D)[N]) {
+CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D)[N],
+                   double (&R)[N]) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -166,6 +169,8 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N],
       for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
       ok = ok && (d > 0.0);
       D[j] = d;
+      const double r = 1.0 / d;
+      R[j] = r;
       L[j][j] = 1.0;
 #pragma unroll
       for (int i = j + 1; i < N; ++i) {
@@ -173,7 +178,7 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N],
           double sacc = M[i][j];
 #pragma unroll
           for (int k = 0; k < j; ++k) sacc = sacc - (L[i][k] * L[j][k]) * D[k];
-          L[i][j] = sacc / d;
+          L[i][j] = sacc * r;
         }
       }
     }
@@ -181,32 +186,31 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N],
   return ok;
 }
 
+// x = (L D L')^-1 b on the leading K entries, with the scaled forward vector
+// zz = D^-1 L^-1 b (or_qp.c ldl_solve); entries from K on are zero.  Each
+// forward step is one block under `i < K`, so a wave skips the steps past the
+// largest working set among its lanes; every computed entry has the
+// arithmetic of the plain loops, bit for bit.
 template <int N>
-CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
-                                            const double (&b)[N], double (&x)[N]) {
-  // forward (L y = b), scale (z = y / D), backward (L' x = z) on the leading
-  // K entries; the entries from K on are zero.  Each forward step and its
-  // division is one block under `i < K`, so a wave skips the steps (and the
-  // divisions) past the largest working set among its lanes (iterate K = 9
-  // at 131 072 QPs -4 %); every computed entry has the arithmetic of the
-  // plain three loops (or_qp.c ldl_solve), bit for bit.
-  double y[N], z[N];
+CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
+                         const double (&b)[N], double (&x)[N], double (&zz)[N]) {
+  double y[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     y[i] = 0.0;
-    z[i] = 0.0;
+    zz[i] = 0.0;
     if (i < K) {
       double v = b[i];
 #pragma unroll
       for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
       y[i] = v;
-      z[i] = v / D[i];
+      zz[i] = v * R[i];
     }
   }
 #pragma unroll
   for (int i = N - 1; i >= 0; --i) {
     if (i < K) {
-      double v = z[i];
+      double v = zz[i];
 #pragma unroll
       for (int k = i + 1; k < N; ++k)
         if (k < K) v = v - L[k][i] * x[k];
@@ -216,8 +220,15 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&D)[N],
     }
   }
 }
+template <int N>
+CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
+                         const double (&b)[N], double (&x)[N]) {
+  double zz[N];
+  ldl_solve_k<N>(K, L, R, b, x, zz);
+}
 
-// (re)build h, M = N' Hinv N and its LDL' for the current working set
+// warm start: M (M[i][k] = n_k' Hinv n_i, k <= i) of the current slots and
+// its LDL' (or_qp.c wset_factor)
 template <int N, bool SN, class Q>
 CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
   double M[N][N];
@@ -237,52 +248,77 @@ CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
         wset_normal(q, W, a, na);
         v = ndot<N>(na, hb);
       }
-      M[a][b] = v;
       M[b][a] = v;
     }
   }
-  return ldl_k<N>(W.K, M, W.L, W.D);
+  return ldl_k<N>(W.K, M, W.L, W.D, W.R);
 }
 
+// remove slot a (or_qp.c wset_remove): the other slots keep their order; the
+// trailing block of the factor takes the rank-one term D_a w w' (GGMS method
+// C1, reciprocal pivots), then rows and columns after a move up by one
 template <int N, bool SN>
 CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
+  double w[N];
+  double alpha = 0.0;
 #pragma unroll
-  for (int b = 0; b + 1 < N; ++b)
-    if (b >= a && b + 1 < W.K) {
-      W.j[b] = W.j[b + 1];
-      W.side[b] = W.side[b + 1];
-      W.lam[b] = W.lam[b + 1];
-      W.bta[b] = W.bta[b + 1];
+  for (int c = 0; c < N; ++c)
+    if (c == a) alpha = W.D[c];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double v = 0.0;
+#pragma unroll
+    for (int c = 0; c < i; ++c)
+      if (c == a) v = W.L[i][c];
+    w[i] = v;
+  }
+#pragma unroll
+  for (int j = 1; j < N; ++j) {
+    if (j > a && j < W.K) {
+      const double p = w[j];
+      const double t = alpha * p;
+      const double d = W.D[j] + t * p;
+      const double r = 1.0 / d;
+      const double bt = t * r;
+      alpha = alpha * (W.D[j] * r);
+      W.D[j] = d;
+      W.R[j] = r;
+#pragma unroll
+      for (int i = j + 1; i < N; ++i)
+        if (i < W.K) {
+          w[i] = w[i] - p * W.L[i][j];
+          W.L[i][j] = W.L[i][j] + bt * w[i];
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i + 1 < N; ++i)
+    if (i >= a && i + 1 < W.K) {
+      W.j[i] = W.j[i + 1];
+      W.side[i] = W.side[i + 1];
+      W.lam[i] = W.lam[i + 1];
+      W.bta[i] = W.bta[i + 1];
+      W.D[i] = W.D[i + 1];
+      W.R[i] = W.R[i + 1];
       if constexpr (SN) {
 #pragma unroll
-        for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b + 1][c];
+        for (int c = 0; c < N; ++c) W.nrm[i][c] = W.nrm[i + 1][c];
       }
+#pragma unroll
+      for (int k = 0; k < i; ++k) W.L[i][k] = (k < a) ? W.L[i + 1][k] : W.L[i + 1][k + 1];
+      W.L[i][i] = 1.0;
     }
   W.K--;
 }
 
-// sorted insert (phase B adds; the warm start fills slots directly)
+// append (j, side) as slot K (or_qp.c wset_append): the bordered factor's
+// row zz = D^-1 L^-1 qv and pivot zn (= den - qv' M^-1 qv), R = 1/zn
 template <int N, bool SN>
-CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double (&n)[N], double bta) {
-  int pos = 0;
+CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double (&n)[N], double bta,
+                      const double (&zz)[N], double zn, double rzn) {
 #pragma unroll
   for (int b = 0; b < N; ++b)
-    if (b < W.K && W.j[b] < j) pos = b + 1;
-#pragma unroll
-  for (int b = N - 1; b > 0; --b)
-    if (b > pos && b <= W.K) {
-      W.j[b] = W.j[b - 1];
-      W.side[b] = W.side[b - 1];
-      W.lam[b] = W.lam[b - 1];
-      W.bta[b] = W.bta[b - 1];
-      if constexpr (SN) {
-#pragma unroll
-        for (int c = 0; c < N; ++c) W.nrm[b][c] = W.nrm[b - 1][c];
-      }
-    }
-#pragma unroll
-  for (int b = 0; b < N; ++b)
-    if (b == pos) {
+    if (b == W.K) {
       W.j[b] = j;
       W.side[b] = side;
       W.lam[b] = lam;
@@ -291,6 +327,11 @@ CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double 
 #pragma unroll
         for (int c = 0; c < N; ++c) W.nrm[b][c] = n[c];
       }
+#pragma unroll
+      for (int k = 0; k < b; ++k) W.L[b][k] = zz[k];
+      W.L[b][b] = 1.0;
+      W.D[b] = zn;
+      W.R[b] = rzn;
     }
   W.K++;
 }
@@ -312,17 +353,18 @@ CMPC_HD void trace_push(QpOut& o, int add, int j, int side) {
   }
 }
 
-// Hinv = H^-1 via LDL' (oracle/or_qp.c step 0).  Returns false if not PD.
+// Hinv = H^-1 via LDL' with reciprocal pivots (oracle/or_qp.c step 0).
+// Returns false if not PD.
 template <int N, class HS>
 CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
-  double L[N][N], D[N];
-  if (!ldl_k<N>(N, H, L, D)) return false;
+  double L[N][N], D[N], R[N];
+  if (!ldl_k<N>(N, H, L, D, R)) return false;
 #pragma unroll
   for (int c = 0; c < N; ++c) {
     double e[N], colv[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) e[i] = (i == c) ? 1.0 : 0.0;
-    ldl_solve_k<N>(N, L, D, e, colv);
+    ldl_solve_k<N>(N, L, R, e, colv);
 #pragma unroll
     for (int i = 0; i <= c; ++i) Hinv.set(i, c, colv[i]);
   }
@@ -339,11 +381,13 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
 // CACHE = true (the Jacobi loop of the iterate kernel): the caller keeps the
 // working set of the previous solve of the same QP (same H, other g) in *wc,
 // with *wc_ws its working-set word, or kWsInvalid.  When ws_in equals it, the
-// warm start takes the slots and the LDL' factors of M = N' H^-1 N from *wc
-// instead of rebuilding them: the same values (a deterministic function of H
-// and the working set), so the result and the trace are bit-identical to the
-// uncached solve.  *wc_ws is set only after a solve that ends OK with its
-// factors matching its slots.
+// warm start takes the slots and the LDL' factor of M = N' H^-1 N from *wc
+// instead of rebuilding them: the same values (the warm start's slot order
+// and full factor are a deterministic function of H and the working set), so
+// the result and the trace are bit-identical to the uncached solve.  *wc_ws
+// is set only after a solve that ends OK without a working-set change (an
+// update-derived factor, or slots in append order, would differ in rounding
+// from the warm start's fresh factor).
 constexpr uint32_t kWsInvalid = 0xFFFFFFFFu;
 
 template <bool TRACE, bool CACHE = false, int N, int NU, int NB, class HS>
@@ -354,7 +398,6 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   WSet<N>& W = CACHE ? *wc : Wl;
   constexpr bool SN = (N <= CMPC_WSET_STORE_MAX);
   const bool cached = CACHE && pd && *wc_ws == ws_in;
-  bool fact_ok = cached;  // W.L, W.D are the factors of the current slots
   o.status = CMPC_QP_OK;
   o.nchg = 0;
   o.ntrace = 0;
@@ -383,7 +426,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     xu[i] = -sacc;
   }
   // A. warm start: slot a = the a-th active constraint of ws_in in ascending
-  // j (the oracle adds them in that order while K < n)
+  // j (the oracle adds them in that order while K < n), then the full factor
   if (!cached) {
     uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
 #pragma unroll
@@ -400,16 +443,12 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         W.K = a + 1;
       }
     }
-  }
-  for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
-    if (!(fact_ok && it == 0)) {
-      fact_ok = wset_factor<N>(q, W);
-      if (!fact_ok) {
-        W.K = 0;
-        ++chg;
-        continue;
-      }
+    if (W.K > 0 && !wset_factor<N>(q, W)) {  // inconsistent warm start: cold
+      W.K = 0;
+      ++chg;
     }
+  }
+  for (int it = 0; it <= N && !done; ++it) {
     double rhs[N];
 #pragma unroll
     for (int a = 0; a < N; ++a) {
@@ -420,7 +459,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         rhs[a] = W.bta[a] - ndot<N>(na, xu);
       }
     }
-    ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
+    ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
     if (CMPC_QP_ABL == 2) break;
     int worst = -1;
     double wv = -tol_d;
@@ -440,7 +479,6 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       }
     if (TRACE) trace_push(o, 0, wj, wsd);
     wset_drop<N>(W, worst);
-    fact_ok = false;
     if (++chg > max_chg) {
       o.status = CMPC_QP_MAX_NWSR;
       done = true;
@@ -502,7 +540,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     const double bp = q.beta(pj, ps);
     double up = 0.0;
     for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
-      double hp[N], qv[N], rv[N], z[N];
+      double hp[N], qv[N], rv[N], zz[N], z[N];
       q.hinv_n(np_, hp);
 #pragma unroll
       for (int a = 0; a < N; ++a) {
@@ -513,7 +551,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
           qv[a] = ndot<N>(na, hp);
         }
       }
-      ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
+      ldl_solve_k<N>(W.K, W.L, W.R, qv, rv, zz);
 #pragma unroll
       for (int r = 0; r < N; ++r) z[r] = hp[r];
 #pragma unroll
@@ -563,11 +601,11 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
           done = true;
           break;
         }
-        fact_ok = wset_factor<N>(q, W);
         continue;
       }
+      const double rzn = 1.0 / zn;
       const double sl = ndot<N>(np_, x) - bp;
-      const double t2 = -sl / zn;
+      const double t2 = -sl * rzn;
       const bool full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
 #pragma unroll
@@ -578,13 +616,11 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       up = up + t;
       if (full) {
         if (TRACE) trace_push(o, 1, pj, ps);
-        wset_add<N>(W, pj, ps, up, np_, bp);
+        wset_add<N>(W, pj, ps, up, np_, bp, zz, zn, rzn);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
           done = true;
-          break;
         }
-        fact_ok = wset_factor<N>(q, W);
         break;
       }
       int kj = 0, ks = 0;
@@ -601,7 +637,6 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         done = true;
         break;
       }
-      fact_ok = wset_factor<N>(q, W);
     }
   }
   o.nchg = chg;
@@ -610,7 +645,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   for (int a = 0; a < N; ++a)
     if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
   o.ws = w;
-  if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && fact_ok) ? w : kWsInvalid;
+  if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && chg == 0) ? w : kWsInvalid;
   // a non-finite plan (a NaN or infinite gradient) fails like any other
   // non-success: zero move (or_qp.c; checked before the bound fixing).  The
   // cached factors stay valid: they depend on H and the working set only.

@@ -1,18 +1,23 @@
 // Row-parallel form of the QP solver (qp_solver.h) for batches too small to
 // fill the GPU with one QP per lane: one QP per 16-lane DPP row, four per
-// wave64.  Same specification and arithmetic order as qp_solve_t and
-// oracle/or_qp.c, bit for bit:
-//  - the O(N^2) products (H^-1 g, H^-1 nu, the LDL' rows of H and the
-//    columns of H^-1) are formed row-parallel: lane l computes entry l with
-//    exactly the operations the scalar code performs for that entry;
-//  - their results are all-gathered inside the row (row_newbcast DPP moves),
-//    and everything else -- the working set, the K x K LDL' of N'H^-1 N, the
-//    multipliers, the ratio tests, the phase-B scan, the iterate x -- runs
-//    replicated in every lane of the row on identical values, so all lanes
-//    of a row take the same branches (a wave diverges over its four QPs, not
-//    over 64).
-// Lane l = lane & 15 of a row: l < N owns row l of H^-1 and entry l of the
-// distributed vectors; lanes N..15 run the replicated code on zero rows.
+// wave64.  Same specification (oracle/or_qp.c, version 2) and arithmetic
+// order as qp_solve_t, bit for bit:
+//  - vectors stay distributed: lane l < N holds row l of H^-1 (registers and
+//    this QP's N x N LDS scratch T), and entry l of x_u, x, H^-1 nu_p, z;
+//  - a column of H^-1 (h_j = H^-1 nall_j, one or two LDS reads per lane) and
+//    a constraint value nu_j' v of a distributed v (one or two ds_bpermute
+//    reads of lanes j, j - nu) take the runtime constraint index directly,
+//    with exactly the scalar code's operations (a single subtraction, a
+//    negation);
+//  - the phase-B scan is lane-parallel: lane c < 2N evaluates constraint c
+//    (both sides), a row ballot tells whether any is violated and a DPP
+//    butterfly min + lowest-lane ballot picks the most violated, first in
+//    (j, side) order on ties, as the scalar scan does;
+//  - the working set and its K x K LDL' factor (append / removal updates of
+//    qp_solver.h) are replicated in every lane of the row on identical
+//    values, so all lanes of a row take the same branches (a wave diverges
+//    over its four QPs, not over 64).
+// Lanes N..15 hold zero rows and run the replicated code on them.
 #pragma once
 #include <type_traits>
 
@@ -23,6 +28,14 @@ template <int L>
 __device__ __forceinline__ double rbc(double v) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + L, 0xF, 0xF, true);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + L, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+// v of a lane of the same row selected by a DPP control (row_shr, quad_perm,
+// mirrors); bound_ctrl: lanes without a source read 0
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 // o[c] = v of lane c of the row, c < N
@@ -52,24 +65,17 @@ struct NoHinv {
 template <int N, int NU>
 using RowQp = Qp<N, NU, NU, NoHinv>;
 
-// entry l of H^-1 n (Qp::hinv_n for row l): hr = row l of H^-1
-template <int N>
-__device__ __forceinline__ double hinv_n_row(const double (&hr)[N], const double (&n)[N]) {
-  double t = 0.0;
-#pragma unroll
-  for (int c = 0; c < N; ++c) t = fma(hr[c], n[c], t);
-  return t;
-}
-
-// H^-1 (hinv_of: LDL' of H, then one ldl_solve per column, the upper
-// triangle from the column solves mirrored).  Hl = row l of H.  The LDL' runs
-// row-parallel (lane i forms L[i][j]; row j of L is broadcast once it is
-// complete and kept, so every lane ends with all of L); lane c then solves
-// column c; the transpose to rows goes through this QP's N x N LDS scratch t.
-// Returns false if H is not positive definite (every lane the same).
+// H^-1 (hinv_of: LDL' of H with reciprocal pivots, then one ldl_solve per
+// column, the upper triangle from the column solves mirrored).  Hl = row l of
+// H.  The LDL' runs row-parallel (lane i forms L[i][j]; row j of L is
+// broadcast once it is complete and kept, so every lane ends with all of L);
+// lane c then solves column c into this QP's N x N LDS scratch t
+// (t[i * N + c] = column c's entry i), which stays valid for the QP's solves
+// (hinv_at); hr = row l of H^-1.  Returns false if H is not positive definite
+// (every lane the same).
 template <int N>
 __device__ __forceinline__ bool hinv_row(const double (&Hl)[N], int l, double (&hr)[N], double* t) {
-  double Li[N], Lf[N][N], D[N];
+  double Li[N], Lf[N][N], D[N], R[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) Li[k] = 0.0;
   bool ok = true;
@@ -84,18 +90,19 @@ __device__ __forceinline__ bool hinv_row(const double (&Hl)[N], int l, double (&
       if (k < j) d = d - (Lf[j][k] * Lf[j][k]) * D[k];
     ok = ok && (d > 0.0);
     D[j] = d;
+    R[j] = 1.0 / d;
     Lf[j][j] = 1.0;
     double sacc = Hl[j];  // M[i][j] of lane i
 #pragma unroll
     for (int k = 0; k < N; ++k)
       if (k < j) sacc = sacc - (Li[k] * Lf[j][k]) * D[k];
-    if (l > j) Li[j] = sacc / d;
+    if (l > j) Li[j] = sacc * R[j];
   });
-  // column l of H^-1 (ldl_solve_k(N, L, D, e_l)): entries i <= l are H^-1(i, l)
+  // column l of H^-1 (ldl_solve_k(N, L, R, e_l)): entries i <= l are H^-1(i, l)
   double e[N], colv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) e[i] = (i == l) ? 1.0 : 0.0;
-  ldl_solve_k<N>(N, Lf, D, e, colv);
+  ldl_solve_k<N>(N, Lf, R, e, colv);
   if (l < N) {
 #pragma unroll
     for (int i = 0; i < N; ++i) t[i * N + l] = colv[i];  // t[i][c] = column c's entry i
@@ -107,48 +114,140 @@ __device__ __forceinline__ bool hinv_row(const double (&Hl)[N], int l, double (&
   // for c < l (hinv_of's mirror)
 #pragma unroll
   for (int c = 0; c < N; ++c) hr[c] = (l >= N) ? 0.0 : (c >= l ? t[l * N + c] : colv[c]);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();  // t is reused by the next QP of this row
   return ok;
 }
 
-// (re)build M = N' H^-1 N and its LDL' for the current working set
-// (wset_factor): H^-1 n_b row-parallel, gathered, the ndots replicated
+// H^-1(r, c) of the specification (upper triangle of the column solves,
+// mirrored) from the LDS scratch t of hinv_row; r < N
+template <int N>
+__device__ __forceinline__ double hinv_at(const double* t, int r, int c) {
+  return r <= c ? t[r * N + c] : t[c * N + r];
+}
+
+// entry l of h = H^-1 nu_{j,side} (or_qp.c hinv_nu): a column, or a
+// difference of two columns, of H^-1; 0 on lanes l >= N
 template <int N, int NU>
-__device__ __forceinline__ bool wset_factor_row(const RowQp<N, NU>& q, const double (&hr)[N],
-                                                WSet<N, false>& W) {
-  double M[N][N];
+__device__ __forceinline__ double hval(const double* t, int l, int j, int side) {
+  if (l >= N) return 0.0;
+  const bool rate = j >= N;
+  const int i = rate ? j - N : j;
+  double v = hinv_at<N>(t, l, i);
+  if (rate && i >= NU) v = v - hinv_at<N>(t, l, i - NU);
+  return side ? -v : v;
+}
+
+// v of lane `src` of this lane's row (ds_bpermute; src runtime)
+__device__ __forceinline__ double row_read(double v, int rowbase, int src) {
+  return __shfl(v, rowbase + src, 64);
+}
+
+// nu_{j,side}' v for a distributed v (entry r in lane r), replicated in the
+// row (or_qp.c nu_dot)
+template <int N, int NU>
+__device__ __forceinline__ double nval(double v, int rowbase, int j, int side) {
+  const bool rate = j >= N;
+  const int i = rate ? j - N : j;
+  double t = row_read(v, rowbase, i);
+  if (rate && i >= NU) t = t - row_read(v, rowbase, i - NU);
+  return side ? -t : t;
+}
+
+// warm start: the LDL' of M (M[i][k] = n_k' h_i, k <= i; wset_factor) with
+// the h_i distributed (hv[i] = entry l of h_i) and M's entries formed where
+// the factorisation reads them, in ldl_k's order
+template <int N, int NU>
+__device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowbase, WSet<N, false>& W) {
+  double hv[N];
 #pragma unroll
-  for (int b = 0; b < N; ++b) {
-    double hb[N];
+  for (int i = 0; i < N; ++i) hv[i] = (i < W.K) ? hval<N, NU>(t, l, W.j[i], W.side[i]) : 0.0;
+  bool ok = true;
 #pragma unroll
-    for (int c = 0; c < N; ++c) hb[c] = 0.0;
-    if (b < W.K) {
-      double nb[N];
-      q.normal(W.j[b], W.side[b], nb);
-      row_gather<N>(hinv_n_row<N>(hr, nb), hb);
-    }
+  for (int j = 0; j < N; ++j) {
+    if (j < W.K) {
+      double d = nval<N, NU>(hv[j], rowbase, W.j[j], W.side[j]);
 #pragma unroll
-    for (int a = 0; a <= b; ++a) {
-      double v = 0.0;
-      if (b < W.K) {
-        double na[N];
-        q.normal(W.j[a], W.side[a], na);
-        v = ndot<N>(na, hb);
+      for (int k = 0; k < j; ++k) d = d - (W.L[j][k] * W.L[j][k]) * W.D[k];
+      ok = ok && (d > 0.0);
+      W.D[j] = d;
+      const double r = 1.0 / d;
+      W.R[j] = r;
+      W.L[j][j] = 1.0;
+#pragma unroll
+      for (int i = j + 1; i < N; ++i) {
+        if (i < W.K) {
+          double sacc = nval<N, NU>(hv[i], rowbase, W.j[j], W.side[j]);
+#pragma unroll
+          for (int k = 0; k < j; ++k) sacc = sacc - (W.L[i][k] * W.L[j][k]) * W.D[k];
+          W.L[i][j] = sacc * r;
+        }
       }
-      M[a][b] = v;
-      M[b][a] = v;
     }
   }
-  return ldl_k<N>(W.K, M, W.L, W.D);
+  return ok;
+}
+
+// Per-QP constants of the lane-parallel scan: lane c < 2N evaluates
+// constraint c (c < N: bound on x_c; else rate row c - N); bounds and
+// thresholds of its two sides (Qp::beta, Qp::thr)
+struct RowScan {
+  double blo, bhi, tlo, thi;  // beta of side 0 / 1, -TOL_P (1 + |beta|)
+  bool live;                  // c < 2N
+};
+template <int N, int NU>
+__device__ __forceinline__ RowScan row_scan_consts(const RowQp<N, NU>& q, int l) {
+  RowScan s;
+  s.live = l < 2 * N;
+  const int j = s.live ? l : 0;
+  s.blo = q.beta(j, 0);
+  s.bhi = q.beta(j, 1);
+  s.tlo = q.thr(j, 0);
+  s.thi = q.thr(j, 1);
+  return s;
+}
+
+// the most violated inactive constraint (phase-B scan of qp_solve_t):
+// returns pj (-1: none) and its side ps, replicated in the row
+template <int N, int NU>
+__device__ __forceinline__ int row_scan(double x_l, const RowScan& sc, uint32_t act, int l, int rowbase,
+                                        int& ps) {
+  // constraint value nu_c' x of lane c: x_c, x_i or x_i - x_{i-NU} (i = c - N)
+  const double xs = dpp64<0x110 + N>(x_l);  // row_shr:N  -> x_{c - N}
+  double v = l < N ? x_l : xs;
+  if constexpr (N > NU) {
+    const double xs2 = dpp64<0x110 + N + NU>(x_l);  // row_shr:N+NU -> x_{c - N - NU}
+    if (l >= N + NU) v = xs - xs2;
+  }
+  const bool inact = sc.live && !((act >> (l & 31)) & 1u);
+  const double slo = v - sc.blo;
+  const double shi = -v - sc.bhi;
+  const bool vlo = inact && slo < sc.tlo;
+  const bool vhi = inact && shi < sc.thi;
+  const unsigned long long any = __ballot(vlo || vhi);
+  ps = 0;
+  if (((any >> rowbase) & 0xFFFFull) == 0) return -1;
+  // the lane's candidate (lower side first on ties), +inf if none
+  const bool takelo = vlo && (!vhi || slo <= shi);
+  const int side = takelo ? 0 : 1;
+  double val = takelo ? slo : (vhi ? shi : __builtin_huge_val());
+  double m = val;
+  m = fmin(m, dpp64<0xB1>(m));   // quad_perm [1,0,3,2]
+  m = fmin(m, dpp64<0x4E>(m));   // quad_perm [2,3,0,1]
+  m = fmin(m, dpp64<0x141>(m));  // row_half_mirror
+  m = fmin(m, dpp64<0x140>(m));  // row_mirror
+  const unsigned long long win = __ballot((vlo || vhi) && val == m);
+  const int pj = __builtin_ctzll((win >> rowbase) & 0xFFFFull);
+  ps = __shfl(side, rowbase + pj, 64);
+  return pj;
 }
 
 // qp_solve_t<TRACE, CACHE = false> for the QP of this row: g_l = entry l of
-// the gradient; x (replicated) = the solution (zero on failure).
+// the gradient, t = hinv_row's LDS scratch, hr = row l of H^-1, sc the scan
+// constants; x_l = entry l of the solution (zero on failure).
 template <bool TRACE, int N, int NU>
-__device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double (&hr)[N], int l, bool pd,
-                                             double tol_d, double g_l, uint32_t ws_in, int max_chg,
-                                             double (&X)[N], QpOut& o) {
+__device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double (&hr)[N], const double* t,
+                                             const RowScan& sc, int l, bool pd, double tol_d, double g_l,
+                                             uint32_t ws_in, int max_chg, double& x_l, QpOut& o) {
+  const int rowbase = (int)(__lane_id() & ~15u);
   WSet<N, false> W;
   o.status = CMPC_QP_OK;
   o.nchg = 0;
@@ -163,20 +262,20 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
   }
   int chg = 0;
   bool done = false;
-  bool fact_ok = false;
   if (!pd) {
     o.status = CMPC_QP_NOT_PD;
     done = true;
   }
-  double G[N], XU[N];
-  row_gather<N>(g_l, G);
+  double xu_l;
   {
+    double G[N];
+    row_gather<N>(g_l, G);
     double sacc = 0.0;
 #pragma unroll
     for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * G[j];
-    row_gather<N>(-sacc, XU);
+    xu_l = -sacc;
   }
-  // A. warm start
+  // A. warm start: slots in ascending j, the full factor
   {
     uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
 #pragma unroll
@@ -192,27 +291,16 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
         W.K = a + 1;
       }
     }
-  }
-  for (int it = 0; it <= 2 * N + 2 && !done; ++it) {
-    if (!(fact_ok && it == 0)) {
-      fact_ok = wset_factor_row<N, NU>(q, hr, W);
-      if (!fact_ok) {
-        W.K = 0;
-        ++chg;
-        continue;
-      }
+    if (W.K > 0 && !wset_factor_row<N, NU>(t, l, rowbase, W)) {  // inconsistent warm start: cold
+      W.K = 0;
+      ++chg;
     }
+  }
+  for (int it = 0; it <= N && !done; ++it) {
     double rhs[N];
 #pragma unroll
-    for (int a = 0; a < N; ++a) {
-      rhs[a] = 0.0;
-      if (a < W.K) {
-        double na[N];
-        q.normal(W.j[a], W.side[a], na);
-        rhs[a] = W.bta[a] - ndot<N>(na, XU);
-      }
-    }
-    ldl_solve_k<N>(W.K, W.L, W.D, rhs, W.lam);
+    for (int a = 0; a < N; ++a) rhs[a] = (a < W.K) ? W.bta[a] - nval<N, NU>(xu_l, rowbase, W.j[a], W.side[a]) : 0.0;
+    ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
     int worst = -1;
     double wv = -tol_d;
 #pragma unroll
@@ -231,87 +319,42 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
       }
     if (TRACE) trace_push(o, 0, wj, wsd);
     wset_drop<N>(W, worst);
-    fact_ok = false;
     if (++chg > max_chg) {
       o.status = CMPC_QP_MAX_NWSR;
       done = true;
     }
   }
-#pragma unroll
-  for (int r = 0; r < N; ++r) X[r] = 0.0;
+  x_l = 0.0;
   if (!done) {
-    // x = xu + sum_a lam_a h_a (per entry, a ascending): entry l here, then gathered
-    double xl = sel<N>(XU, l);
+    // x = xu + sum_a lam_a h_a (entry l, a ascending)
+    x_l = xu_l;
 #pragma unroll
-    for (int a = 0; a < N; ++a) {
-      if (a < W.K) {
-        double na[N];
-        q.normal(W.j[a], W.side[a], na);
-        xl = xl + W.lam[a] * hinv_n_row<N>(hr, na);
-      }
-    }
-    row_gather<N>(xl, X);
+    for (int a = 0; a < N; ++a)
+      if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
   }
   // B. Goldfarb–Idnani
   for (int outer = 0; outer <= max_chg + 1 && !done; ++outer) {
-    int pj = -1, ps = 0;
-    double pv = 0.0;
-    bool anyv = false;
+    uint32_t act = 0;
 #pragma unroll
-    for (int j = 0; j < 2 * N; ++j)
-#pragma unroll
-      for (int sd = 0; sd < 2; ++sd) anyv = anyv | (q.nu_dot(j, sd, X) - q.beta(j, sd) < q.thr(j, sd));
-    if (anyv) {
-      uint32_t act = 0;
-#pragma unroll
-      for (int a = 0; a < N; ++a)
-        if (a < W.K) act |= 1u << W.j[a];
-#pragma unroll
-      for (int j = 0; j < 2 * N; ++j) {
-        if (!((act >> j) & 1u)) {
-#pragma unroll
-          for (int sd = 0; sd < 2; ++sd) {
-            const double sl = q.nu_dot(j, sd, X) - q.beta(j, sd);
-            if (sl < q.thr(j, sd) && (pj < 0 || sl < pv)) {
-              pj = j;
-              ps = sd;
-              pv = sl;
-            }
-          }
-        }
-      }
-    }
+    for (int a = 0; a < N; ++a)
+      if (a < W.K) act |= 1u << W.j[a];
+    int ps = 0;
+    const int pj = row_scan<N, NU>(x_l, sc, act, l, rowbase, ps);
     if (pj < 0) break;  // optimal
-    double np_[N];
-    q.normal(pj, ps, np_);
     const double bp = q.beta(pj, ps);
+    const double hp_l = hval<N, NU>(t, l, pj, ps);
     double up = 0.0;
     for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
-      double HP[N], qv[N], rv[N], Z[N];
-      const double hp_l = hinv_n_row<N>(hr, np_);
-      row_gather<N>(hp_l, HP);
+      double qv[N], rv[N], zz[N];
 #pragma unroll
-      for (int a = 0; a < N; ++a) {
-        qv[a] = 0.0;
-        if (a < W.K) {
-          double na[N];
-          q.normal(W.j[a], W.side[a], na);
-          qv[a] = ndot<N>(na, HP);
-        }
-      }
-      ldl_solve_k<N>(W.K, W.L, W.D, qv, rv);
-      double zl = hp_l;
+      for (int a = 0; a < N; ++a) qv[a] = (a < W.K) ? nval<N, NU>(hp_l, rowbase, W.j[a], W.side[a]) : 0.0;
+      ldl_solve_k<N>(W.K, W.L, W.R, qv, rv, zz);
+      double z_l = hp_l;
 #pragma unroll
-      for (int a = 0; a < N; ++a) {
-        if (a < W.K) {
-          double na[N];
-          q.normal(W.j[a], W.side[a], na);
-          zl = zl - rv[a] * hinv_n_row<N>(hr, na);
-        }
-      }
-      row_gather<N>(zl, Z);
-      const double zn = ndot<N>(np_, Z);
-      const double den = ndot<N>(np_, HP);
+      for (int a = 0; a < N; ++a)
+        if (a < W.K) z_l = z_l - rv[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+      const double zn = nval<N, NU>(z_l, rowbase, pj, ps);
+      const double den = nval<N, NU>(hp_l, rowbase, pj, ps);
       int k = -1;
       double t1 = 0.0;
 #pragma unroll
@@ -347,28 +390,26 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
           done = true;
           break;
         }
-        fact_ok = wset_factor_row<N, NU>(q, hr, W);
         continue;
       }
-      const double sl = ndot<N>(np_, X) - bp;
-      const double t2 = -sl / zn;
+      const double rzn = 1.0 / zn;
+      const double sl = nval<N, NU>(x_l, rowbase, pj, ps) - bp;
+      const double t2 = -sl * rzn;
       const bool full = (k < 0) || (t2 <= t1);
-      const double t = full ? t2 : t1;
-#pragma unroll
-      for (int r = 0; r < N; ++r) X[r] = X[r] + t * Z[r];
+      const double tt = full ? t2 : t1;
+      x_l = x_l + tt * z_l;
 #pragma unroll
       for (int a = 0; a < N; ++a)
-        if (a < W.K) W.lam[a] = W.lam[a] - t * rv[a];
-      up = up + t;
+        if (a < W.K) W.lam[a] = W.lam[a] - tt * rv[a];
+      up = up + tt;
       if (full) {
         if (TRACE) trace_push(o, 1, pj, ps);
-        wset_add<N>(W, pj, ps, up, np_, bp);
+        double nz[N];  // (unused: the row form keeps no normals)
+        wset_add<N>(W, pj, ps, up, nz, bp, zz, zn, rzn);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
           done = true;
-          break;
         }
-        fact_ok = wset_factor_row<N, NU>(q, hr, W);
         break;
       }
       int kj = 0, ks = 0;
@@ -385,7 +426,6 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
         done = true;
         break;
       }
-      fact_ok = wset_factor_row<N, NU>(q, hr, W);
     }
   }
   o.nchg = chg;
@@ -394,20 +434,13 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
   for (int a = 0; a < N; ++a)
     if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
   o.ws = w;
-  (void)fact_ok;
   if (o.status == CMPC_QP_OK) {
-    bool fin = true;
-#pragma unroll
-    for (int r = 0; r < N; ++r) fin = fin && __builtin_isfinite(X[r]);
-    if (!fin) o.status = CMPC_QP_NONFINITE;
+    const unsigned long long bad = __ballot(l < N && !__builtin_isfinite(x_l));
+    if ((bad >> rowbase) & 0xFFFFull) o.status = CMPC_QP_NONFINITE;
   }
   if (o.status == CMPC_QP_OK) {
-    const uint32_t bnd = w & ((1u << N) - 1u), upm = (w >> 16) & bnd;
-#pragma unroll
-    for (int r = 0; r < N; ++r)
-      X[r] = ((bnd >> r) & 1u) ? (((upm >> r) & 1u) ? q.ubv(r) : q.lbv(r)) : X[r];
+    if (l < N && ((w >> l) & 1u)) x_l = ((w >> (16 + l)) & 1u) ? q.ubv(l) : q.lbv(l);
   } else {
-#pragma unroll
-    for (int r = 0; r < N; ++r) X[r] = 0.0;
+    x_l = 0.0;
   }
 }

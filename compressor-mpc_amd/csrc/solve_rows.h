@@ -30,10 +30,11 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
 #pragma unroll
   for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
   uint32_t ws = P.ws[q];
-  double dprev[N];  // (without other controllers only the K = 0 output reads it)
+  // the plan, entry l in lane l (without other controllers only the K = 0
+  // output reads it)
+  double dprev_l = 0.0;
   if constexpr (NVO > 0) {
-#pragma unroll
-    for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+    if (own) dprev_l = P.du_old[(size_t)q * N + l];
   }
 #pragma unroll
   for (int c = 0; c < NU; ++c) {
@@ -43,6 +44,7 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
     qp.ubA[c] = cfg[P.co.rupper + c];
   }
   qp.tolerances();
+  const RowScan sc = row_scan_consts<N, NU>(qp, l);
   double hr[N];
   const bool pd = hinv_row<N>(Hl, l, hr, tsh);
   double hmax = 0.0;
@@ -54,16 +56,16 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
   }
   const double tol_d = TOL_D * (1.0 + hmax);
 
-  double x[N];
+  double x_l = 0.0;
   QpOut o;
   if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
-    qp_solve_row<false, N, NU>(qp, hr, l, pd, tol_d, f_l, 0u, CMPC_NWSR_MAX, x, o);
+    qp_solve_row<false, N, NU>(qp, hr, tsh, sc, l, pd, tol_d, f_l, 0u, CMPC_NWSR_MAX, x_l, o);
     if (active && l == 0) P.ws[q] = o.ws;
+    __builtin_amdgcn_wave_barrier();  // tsh is reused by the next QP of this row
     return;
   }
   if constexpr (NVO == 0) {
-#pragma unroll
-    for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
+    if (own) dprev_l = P.du_old[(size_t)q * N + l];
   }
   for (int k = 0; k < P.K; ++k) {
     {  // fair progress of the SIMD's waves (cf. cmpc_solve_kernel)
@@ -86,6 +88,8 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
             for (int c = 0; c < NU; ++c)
               dother[mv * (SM1 * NU) + rk * NU + c] = P.du_other[(size_t)q * NVO + rk * N + mv * NU + c];
       } else {
+        // the other sub-controllers' plans: entry mv * NU + c of sub-controller
+        // s2 sits in lane mv * NU + c of its row
 #pragma unroll
         for (int rk = 0; rk < SM1; ++rk) {
           const int s2 = rk + (rk >= s ? 1 : 0);
@@ -93,17 +97,16 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
           for (int mv = 0; mv < M; ++mv)
 #pragma unroll
             for (int c = 0; c < NU; ++c)
-              dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + 16 * s2 + l, 64);
+              dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev_l, base_lane + 16 * s2 + mv * NU + c, 64);
         }
       }
       // f_k = f + G du_other, entry l (cmpc_solve_kernel's order)
 #pragma unroll
       for (int c = 0; c < NVOA; ++c) fk = fk + Gl[c] * dother[c];
     }
-    qp_solve_row<TRACE, N, NU>(qp, hr, l, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
+    qp_solve_row<TRACE, N, NU>(qp, hr, tsh, sc, l, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x_l, o);
     ws = o.ws;
-#pragma unroll
-    for (int a = 0; a < N; ++a) dprev[a] = x[a];
+    dprev_l = x_l;
     if (TRACE && active && l == 0 && P.trace) {
       uint32_t* tr = reinterpret_cast<uint32_t*>(P.trace + ((size_t)q * P.K + k) * 16);
 #pragma unroll
@@ -111,6 +114,7 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
       P.ntrace[(size_t)q * P.K + k] = o.ntrace;
     }
   }
+  __builtin_amdgcn_wave_barrier();  // tsh is reused by the next QP of this row
   if (!active) return;
   if (l == 0) {
     P.ws[q] = ws;
@@ -120,11 +124,10 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
     }
   }
   if (own) {
-    const double v = sel<N>(dprev, l);
-    P.du[(size_t)q * N + l] = v;
-    P.du_old[(size_t)q * N + l] = v;
+    P.du[(size_t)q * N + l] = dprev_l;
+    P.du_old[(size_t)q * N + l] = dprev_l;
   }
   if ((P.flags & CMPC_APPLY_MOVE) && l < NU) {
-    P.u_old[(size_t)q * P.nu_tot + l] = sel<NU>(uo, l) + sel<N>(dprev, l);
+    P.u_old[(size_t)q * P.nu_tot + l] = sel<NU>(uo, l) + dprev_l;
   }
 }

@@ -2,10 +2,11 @@
  * ORACLE — TEST INFRASTRUCTURE ONLY (never linked into the product).
  *
  * The build's QP solver, restated for the CPU: a warm-started dual
- * (Goldfarb–Idnani) active-set method with dense re-factorisation, standing
- * in for qpOASES 3.2.0 SQProblem::hotstart (libs/mpc_qp_solver.cc:62-72;
- * qpOASES is a CMakeLists.txt:20-23 dependency that the reference does not
- * vendor).  The QP is the reference's
+ * (Goldfarb–Idnani) active-set method whose working-set factorisation is
+ * updated (append / removal) rather than rebuilt, standing in for qpOASES
+ * 3.2.0 SQProblem::hotstart (libs/mpc_qp_solver.cc:62-72; qpOASES is a
+ * CMakeLists.txt:20-23 dependency that the reference does not vendor).  The
+ * QP is the reference's
  *     min 1/2 x'Hx + g'x
  *     s.t. lb <= x <= ub, lbA <= Ain x <= ubA,
  *     Ain = [I 0 ..; -I I 0 ..; ...]     include/mpc_qp_solver.h:108-123
@@ -14,22 +15,35 @@
  * (libs/mpc_qp_solver.cc:66-69), warm start from the previous working set of
  * the same QP slot (hotstart).
  *
- * Algorithm specification (the HIP kernel implements the same steps in the
- * same arithmetic order):
- *   0. Hinv = H^-1 via LDL' (no square roots); any pivot <= 0 -> NOT_PD.
- *      x_u = -Hinv g.
- *   A. Warm start: W = ws_in.  Solve the equality QP on W:
- *      lam = (N'Hinv N)^-1 (beta_W - N' x_u), x = x_u + Hinv N lam.
- *      While some lam_w < -tol_d: drop the most negative (lowest j on ties),
- *      count one change, re-solve.
- *   B. Repeat: pick the most violated constraint p (slack < -tol_p, most
- *      negative; ties -> lowest j, lower side first).  None -> optimal.
- *      Goldfarb–Idnani step loop: r = M^-1 N'Hinv nu_p,
- *      z = Hinv nu_p - Hinv N r, t1 = min_{r_w > tol_r} lam_w / r_w,
- *      t2 = -slack_p / (nu_p' z).  If nu_p'z <= tol_z nu_p'Hinv nu_p
- *      (dependent): no blocking -> INFEASIBLE, else dual step t1 and drop.
- *      Else t = min(t1, t2) (t2 wins ties): x += t z, lam -= t r,
- *      u_p += t; full step adds p, partial step drops the blocker.
+ * Algorithm specification, version 2 (the HIP kernels implement the same
+ * steps in the same arithmetic order):
+ *   0. H = L D L' with reciprocal pivots R = 1/D (any pivot <= 0 -> NOT_PD);
+ *      Hinv column by column from that factor.  x_u = -Hinv g.
+ *      nall_j = the normal of constraint j without its side: e_j (j < n),
+ *      e_i (rate row i = j - n < nu), e_i - e_{i-nu} (rate row i >= nu).
+ *      h_j = Hinv nall_j (a column or a difference of two columns).
+ *   A. Warm start: slots = the constraints of ws_in in ascending j.  The
+ *      working-set matrix M (M[i][k] = s_i s_k nall_{j_k}' h_{j_i} for
+ *      i >= k, s = +1 lower side, -1 upper side) is factored M = L D L',
+ *      reciprocal pivots R; a pivot <= 0 -> cold start (W empty, one change).
+ *      lam = M^-1 (beta_W - N' x_u); while some lam_w < -tol_d: drop the most
+ *      negative (lowest slot on ties) by the factor removal below, count one
+ *      change, re-solve.  x = x_u + sum_a lam_a s_a h_{j_a}.
+ *   B. Repeat: pick the most violated inactive constraint p (slack < -tol_p,
+ *      most negative; ties -> lowest j, lower side first).  None -> optimal.
+ *      Goldfarb–Idnani step loop: hp = s_p h_p, qv = N'hp, r = M^-1 qv (the
+ *      solve's scaled forward vector zz kept), z = hp - sum_a r_a s_a h_a,
+ *      zn = nu_p'z, den = nu_p'hp, t1 = min_{r_a > tol_r} lam_a / r_a.
+ *      If zn <= tol_z den (dependent): no blocking -> INFEASIBLE, else a dual
+ *      step t1 and the blocker is removed.  Else t2 = -slack_p * (1/zn),
+ *      t = min(t1, t2) (t2 wins ties): x += t z, lam -= t r, u_p += t; a full
+ *      step APPENDS p as the last slot (L row = zz, pivot zn, R = 1/zn: the
+ *      bordered factor of [M qv; qv' den]); a partial step removes the
+ *      blocker.
+ *   Factor removal of slot a (order of the other slots kept): rows and pivots
+ *      before a unchanged; rows after a move up one; the trailing block gets
+ *      the rank-one term D_a w w' (w = column a below a) by Gill, Golub,
+ *      Murray & Saunders (1974) method C1 with reciprocal pivots (remove()).
  *   Every add/drop counts one change; the 11th change -> MAX_NWSR.
  *   On success, variables at an active bound are set exactly to that bound.
  *
@@ -47,7 +61,7 @@
  *                over max(1, |r_a|)
  *   dependence   nu_p'z vs TOL_Z nu_p'Hinv nu_p over nu_p'Hinv nu_p
  *   step kind    t2 vs t1 over max(|t1|, |t2|)
- *   factor       working-set LDL' pivots over the diagonal of M
+ *   factor       the warm start's LDL' pivots over the diagonal of M
  * (tests against a tolerance skip a rounding-noise zero: see mg_tol).
  * A QP whose inputs differ from another's by FP64 reassociation only
  * (~1e-13 relative) takes the same decisions whenever its margin is well
@@ -93,34 +107,45 @@ static void mg_tol(qp_t* q, double a, double thr, double scale) {
   if (fabs(a) > 1e-3 * fabs(thr)) mg(q, a, thr, scale);
 }
 
-static int ldl(int n, double M[QMAX][QMAX], double L[QMAX][QMAX],
-               double D[QMAX]) {
+/* LDL' of the leading n x n block of a symmetric M (lower triangle read),
+ * reciprocal pivots R = 1/D:
+ *   d_j = M_jj - sum_{k<j} (L_jk L_jk) D_k,       R_j = 1 / d_j
+ *   L_ij = (M_ij - sum_{k<j} (L_ik L_jk) D_k) R_j  (i > j), k ascending.
+ * Returns -(j+1) for the first pivot d_j <= 0 (the rest still computed). */
+static int ldl(int n, double M[QMAX][QMAX], double L[QMAX][QMAX], double D[QMAX],
+               double R[QMAX]) {
+  int rc = 0;
   for (int j = 0; j < n; ++j) {
     double d = M[j][j];
     for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
     D[j] = d;
-    if (!(d > 0)) return -(j + 1);
+    R[j] = 1.0 / d;
+    if (!(d > 0) && !rc) rc = -(j + 1);
     L[j][j] = 1.0;
     for (int i = j + 1; i < n; ++i) {
       double s = M[i][j];
       for (int k = 0; k < j; ++k) s = s - (L[i][k] * L[j][k]) * D[k];
-      L[i][j] = s / d;
+      L[i][j] = s * R[j];
     }
   }
-  return 0;
+  return rc;
 }
 
-static void ldl_solve(int n, double L[QMAX][QMAX], const double D[QMAX],
-                      const double* b, double* x) {
+/* x = (L D L')^-1 b; also the forward vector y = L^-1 b and the scaled
+ * zz = D^-1 y (the row a bordered factor appends):
+ *   y_i = b_i - sum_{k<i} L_ik y_k,  zz_i = y_i R_i,
+ *   x_i = zz_i - sum_{k>i} L_ki x_k  (k ascending). */
+static void ldl_solve(int n, double L[QMAX][QMAX], const double R[QMAX], const double* b,
+                      double* x, double* zz) {
   double y[QMAX];
   for (int i = 0; i < n; ++i) {
     double v = b[i];
     for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
     y[i] = v;
   }
-  for (int i = 0; i < n; ++i) y[i] = y[i] / D[i];
+  for (int i = 0; i < n; ++i) zz[i] = y[i] * R[i];
   for (int i = n - 1; i >= 0; --i) {
-    double v = y[i];
+    double v = zz[i];
     for (int k = i + 1; k < n; ++k) v = v - L[k][i] * x[k];
     x[i] = v;
   }
@@ -161,21 +186,17 @@ typedef struct {
   int K;
   int j[QMAX], side[QMAX];
   double lam[QMAX];
-  double h[QMAX][QMAX]; /* h[a] = Hinv nu_a */
-  double L[QMAX][QMAX], D[QMAX];
+  double L[QMAX][QMAX], D[QMAX], R[QMAX];
 } wset_t;
 
-/* (re)build h, M = N'Hinv N and its LDL' for the current W */
+/* warm start: M of the current slots and its LDL' */
 static int wset_factor(qp_t* q, wset_t* W) {
-  double M[QMAX][QMAX];
-  for (int a = 0; a < W->K; ++a) hinv_nu(q, W->j[a], W->side[a], W->h[a]);
-  for (int a = 0; a < W->K; ++a)
-    for (int b = a; b < W->K; ++b) {
-      const double v = nu_dot(q, W->j[a], W->side[a], W->h[b]);
-      M[a][b] = v;
-      M[b][a] = v;
-    }
-  const int rc = ldl(W->K, M, W->L, W->D);
+  double M[QMAX][QMAX], h[QMAX];
+  for (int i = 0; i < W->K; ++i) {
+    hinv_nu(q, W->j[i], W->side[i], h);
+    for (int k = 0; k <= i; ++k) M[i][k] = nu_dot(q, W->j[k], W->side[k], h);
+  }
+  const int rc = ldl(W->K, M, W->L, W->D, W->R);
   /* margin of the pivot test d > 0 (pivots relative to M's diagonal), up
    * to and including a failing pivot */
   const int np = rc ? -rc : W->K;
@@ -183,27 +204,57 @@ static int wset_factor(qp_t* q, wset_t* W) {
   return rc;
 }
 
-static void wset_drop(wset_t* W, int a) {
-  for (int b = a; b + 1 < W->K; ++b) {
-    W->j[b] = W->j[b + 1];
-    W->side[b] = W->side[b + 1];
-    W->lam[b] = W->lam[b + 1];
+/* remove slot a: the other slots keep their order; the factor of the
+ * remaining working set by a rank-one update of the trailing block
+ * (GGMS method C1):  alpha = D_a, w_i = L_ia (i > a); for j = a+1.. :
+ *   p = w_j, t = alpha p, d = D_j + t p, r = 1/d, beta = t r,
+ *   alpha = alpha (D_j r), D_j = d, R_j = r;
+ *   for i > j: w_i = w_i - p L_ij, L_ij = L_ij + beta w_i.
+ * Then rows / columns after a move up by one. */
+static void wset_remove(wset_t* W, int a) {
+  double w[QMAX];
+  double alpha = W->D[a];
+  for (int i = a + 1; i < W->K; ++i) w[i] = W->L[i][a];
+  for (int j = a + 1; j < W->K; ++j) {
+    const double p = w[j];
+    const double t = alpha * p;
+    const double d = W->D[j] + t * p;
+    const double r = 1.0 / d;
+    const double bt = t * r;
+    alpha = alpha * (W->D[j] * r);
+    W->D[j] = d;
+    W->R[j] = r;
+    for (int i = j + 1; i < W->K; ++i) {
+      w[i] = w[i] - p * W->L[i][j];
+      W->L[i][j] = W->L[i][j] + bt * w[i];
+    }
+  }
+  for (int i = a; i + 1 < W->K; ++i) {
+    W->j[i] = W->j[i + 1];
+    W->side[i] = W->side[i + 1];
+    W->lam[i] = W->lam[i + 1];
+    W->D[i] = W->D[i + 1];
+    W->R[i] = W->R[i + 1];
+    for (int k = 0; k < a; ++k) W->L[i][k] = W->L[i + 1][k];
+    for (int k = a; k < i; ++k) W->L[i][k] = W->L[i + 1][k + 1];
+    W->L[i][i] = 1.0;
   }
   W->K--;
 }
 
-static void wset_add(wset_t* W, int j, int side, double lam) {
-  int a = W->K;
-  while (a > 0 && W->j[a - 1] > j) {
-    W->j[a] = W->j[a - 1];
-    W->side[a] = W->side[a - 1];
-    W->lam[a] = W->lam[a - 1];
-    --a;
-  }
-  W->j[a] = j;
-  W->side[a] = side;
-  W->lam[a] = lam;
-  W->K++;
+/* append p as the last slot: the bordered factor of [M qv; qv' den] is
+ * L row zz = D^-1 L^-1 qv and pivot den - qv'M^-1 qv = zn */
+static void wset_append(wset_t* W, int j, int side, double lam, const double* zz, double zn,
+                        double rzn) {
+  const int K = W->K;
+  W->j[K] = j;
+  W->side[K] = side;
+  W->lam[K] = lam;
+  for (int k = 0; k < K; ++k) W->L[K][k] = zz[k];
+  W->L[K][K] = 1.0;
+  W->D[K] = zn;
+  W->R[K] = rzn;
+  W->K = K + 1;
 }
 
 static void trace_push(or_qp_info* info, int add, int j, int side) {
@@ -228,19 +279,19 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
   W.K = 0;
   /* 0. Hinv */
   {
-    double Hm[QMAX][QMAX], L[QMAX][QMAX], D[QMAX];
+    double Hm[QMAX][QMAX], L[QMAX][QMAX], D[QMAX], R[QMAX];
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) Hm[i][j] = H[i * n + j];
-    const int rc = ldl(n, Hm, L, D);
+    const int rc = ldl(n, Hm, L, D, R);
     for (int a = 0; a < (rc ? -rc : n); ++a) mg(&q, D[a], 0.0, fabs(H[a * n + a]));
     if (rc) {
       status = CMPC_QP_NOT_PD;
       goto done;
     }
     for (int c = 0; c < n; ++c) {
-      double e[QMAX], col[QMAX];
+      double e[QMAX], col[QMAX], zz[QMAX];
       for (int i = 0; i < n; ++i) e[i] = (i == c) ? 1.0 : 0.0;
-      ldl_solve(n, L, D, e, col);
+      ldl_solve(n, L, R, e, col, zz);
       for (int i = 0; i <= c; ++i) q.Hinv[i][c] = col[i];
     }
     for (int c = 0; c < n; ++c)
@@ -267,19 +318,23 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     q.s_lam = fmax(fmax(sg, (1.0 + hmax) * sx), tol_d);
   }
 
-  /* A. warm start from ws_in */
+  /* A. warm start from ws_in: slots in ascending j */
   for (int j = 0; j < 2 * n; ++j)
-    if ((ws_in & (1u << j)) && W.K < n) wset_add(&W, j, (ws_in >> (16 + j)) & 1u, 0.0);
-  for (;;) {
-    if (wset_factor(&q, &W)) { /* inconsistent warm start: cold */
-      W.K = 0;
-      ++chg;
-      continue;
+    if ((ws_in & (1u << j)) && W.K < n) {
+      W.j[W.K] = j;
+      W.side[W.K] = (ws_in >> (16 + j)) & 1u;
+      W.lam[W.K] = 0.0;
+      W.K++;
     }
-    double rhs[QMAX];
+  while (W.K > 0 && wset_factor(&q, &W)) { /* inconsistent warm start: cold */
+    W.K = 0;
+    ++chg;
+  }
+  for (;;) {
+    double rhs[QMAX], zz[QMAX];
     for (int a = 0; a < W.K; ++a)
       rhs[a] = beta(&q, W.j[a], W.side[a]) - nu_dot(&q, W.j[a], W.side[a], xu);
-    ldl_solve(W.K, W.L, W.D, rhs, W.lam);
+    ldl_solve(W.K, W.L, W.R, rhs, W.lam, zz);
     int worst = -1;
     double wv = -tol_d;
     for (int a = 0; a < W.K; ++a)
@@ -293,16 +348,17 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     }
     if (worst < 0) break;
     trace_push(info, 0, W.j[worst], W.side[worst]);
-    wset_drop(&W, worst);
+    wset_remove(&W, worst);
     if (++chg > max_chg) {
       status = CMPC_QP_MAX_NWSR;
       goto done;
     }
   }
-  for (int r = 0; r < n; ++r) {
-    double v = xu[r];
-    for (int a = 0; a < W.K; ++a) v = v + W.lam[a] * W.h[a][r];
-    x[r] = v;
+  for (int r = 0; r < n; ++r) x[r] = xu[r];
+  for (int a = 0; a < W.K; ++a) {
+    double h[QMAX];
+    hinv_nu(&q, W.j[a], W.side[a], h);
+    for (int r = 0; r < n; ++r) x[r] = x[r] + W.lam[a] * h[r];
   }
 
   /* B. Goldfarb–Idnani */
@@ -336,14 +392,15 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     if (pj < 0) break; /* optimal */
     double up = 0.0;
     for (;;) {
-      double hp[QMAX], qv[QMAX], rv[QMAX], z[QMAX];
+      double hp[QMAX], qv[QMAX], rv[QMAX], zz[QMAX], z[QMAX];
       hinv_nu(&q, pj, ps, hp);
       for (int a = 0; a < W.K; ++a) qv[a] = nu_dot(&q, W.j[a], W.side[a], hp);
-      ldl_solve(W.K, W.L, W.D, qv, rv);
-      for (int r = 0; r < n; ++r) {
-        double v = hp[r];
-        for (int a = 0; a < W.K; ++a) v = v - rv[a] * W.h[a][r];
-        z[r] = v;
+      ldl_solve(W.K, W.L, W.R, qv, rv, zz);
+      for (int r = 0; r < n; ++r) z[r] = hp[r];
+      for (int a = 0; a < W.K; ++a) {
+        double h[QMAX];
+        hinv_nu(&q, W.j[a], W.side[a], h);
+        for (int r = 0; r < n; ++r) z[r] = z[r] - rv[a] * h[r];
       }
       const double zn = nu_dot(&q, pj, ps, z);
       const double den = nu_dot(&q, pj, ps, hp);
@@ -371,16 +428,16 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
         for (int a = 0; a < W.K; ++a) W.lam[a] = W.lam[a] - t1 * rv[a];
         up = up + t1;
         trace_push(info, 0, W.j[k], W.side[k]);
-        wset_drop(&W, k);
+        wset_remove(&W, k);
         if (++chg > max_chg) {
           status = CMPC_QP_MAX_NWSR;
           goto done;
         }
-        wset_factor(&q, &W);
         continue;
       }
+      const double rzn = 1.0 / zn;
       const double sl = nu_dot(&q, pj, ps, x) - beta(&q, pj, ps);
-      const double t2 = -sl / zn;
+      const double t2 = -sl * rzn;
       if (k >= 0) mg(&q, t2, t1, fmax(fabs(t1), fabs(t2)));
       const int full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
@@ -389,21 +446,19 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
       up = up + t;
       if (full) {
         trace_push(info, 1, pj, ps);
-        wset_add(&W, pj, ps, up);
+        wset_append(&W, pj, ps, up, zz, zn, rzn);
         if (++chg > max_chg) {
           status = CMPC_QP_MAX_NWSR;
           goto done;
         }
-        wset_factor(&q, &W);
         break;
       }
       trace_push(info, 0, W.j[k], W.side[k]);
-      wset_drop(&W, k);
+      wset_remove(&W, k);
       if (++chg > max_chg) {
         status = CMPC_QP_MAX_NWSR;
         goto done;
       }
-      wset_factor(&q, &W);
     }
   }
 done:
