@@ -100,6 +100,29 @@ def qp_solve_batch(H, g, lb, ub, lbA, ubA, nu, ws_in=None, max_chg=10, device=0)
     return x, status, nchg, ws_out, trace, ntrace
 
 
+def qp_solve_batch_map(H, f, G, d, lb, ub, lbA, ubA, nu, ws_in=None, max_chg=10, device=0):
+    """One Jacobi-iteration solve per QP in the map form (g = f + G d), the
+    solve of cmpc_iterate / DistributedSolver::UpdateAndSolveQP."""
+    H = np.ascontiguousarray(H, np.float64)
+    nqp, n = f.shape
+    G = np.ascontiguousarray(G, np.float64).reshape(nqp, n, -1)
+    nvo = G.shape[2]
+    c = lambda a: np.ascontiguousarray(a, np.float64)
+    ws_in = np.zeros(nqp, np.uint32) if ws_in is None else np.ascontiguousarray(ws_in, np.uint32)
+    x = np.zeros((nqp, n))
+    status = np.zeros(nqp, np.int32)
+    nchg = np.zeros(nqp, np.int32)
+    ws_out = np.zeros(nqp, np.uint32)
+    trace = np.zeros((nqp, 16), np.uint8)
+    ntrace = np.zeros(nqp, np.int32)
+    lib = load_library()
+    check(lib.cmpc_qp_solve_batch_map(device, n, nu, nvo, nqp, dptr(H), dptr(c(f)), dptr(G), dptr(c(d)),
+                                      dptr(c(lb)), dptr(c(ub)), dptr(c(lbA)), dptr(c(ubA)), uptr(ws_in), max_chg,
+                                      dptr(x), iptr(status), iptr(nchg), uptr(ws_out), bptr(trace), iptr(ntrace)),
+          "cmpc_qp_solve_batch_map")
+    return x, status, nchg, ws_out, trace, ntrace
+
+
 def _torch_runtime_first():
     """torch bundles its own HIP runtime; when the library's runtime opens the
     device first, torch's later initialisation reports no GPUs.  If the

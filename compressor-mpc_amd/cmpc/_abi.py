@@ -96,7 +96,7 @@ EXPORTS = (
     "cmpc_lin_device", "cmpc_build", "cmpc_set_build_variant", "cmpc_rows_lds_model", "cmpc_last_build_kernel", "cmpc_set_solve_variant", "cmpc_last_solve_kernel", "cmpc_set_step_variant", "cmpc_last_step_fused", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
     "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
-    "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_bind_lin",
+    "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_qp_solve_batch_map", "cmpc_bind_lin",
     "cmpc_bind_state",
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate", "cmpc_coupled_validate",
     "cmpc_get_input", "cmpc_get_input_host", "cmpc_update_u", "cmpc_update_u_host",
@@ -228,9 +228,15 @@ def load_library(path: str = LIB_PATH):
                                  P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32), ctypes.c_int,
                                  P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],
                                 ctypes.c_int),
+        "cmpc_qp_solve_batch_map": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(dbl), P(u32),
+                                     ctypes.c_int, P(dbl), P(i32), P(i32), P(u32), P(ctypes.c_uint8), P(i32)],
+                                    ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # (an older library build: A/B timing runs; tests/test_abi.py checks the exports)
+            continue
         fn.argtypes = argtypes
         fn.restype = restype
     _lib = lib

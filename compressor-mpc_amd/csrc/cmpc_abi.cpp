@@ -2088,4 +2088,56 @@ int cmpc_qp_solve_batch(int device, int n, int nu, int nqp, const double* H, con
   return 0;
 }
 
+int cmpc_qp_solve_batch_map(int device, int n, int nu, int nvo, int nqp, const double* H, const double* f,
+                            const double* G, const double* d, const double* lb, const double* ub,
+                            const double* lbA, const double* ubA, const uint32_t* ws_in, int max_chg, double* x,
+                            int32_t* status, int32_t* nchg, uint32_t* ws_out, uint8_t* trace, int32_t* ntrace) {
+  if (nvo == 0)
+    return cmpc_qp_solve_batch(device, n, nu, nqp, H, f, lb, ub, lbA, ubA, ws_in, max_chg, x, status, nchg, ws_out,
+                               trace, ntrace);
+  if (nqp <= 0) return 0;
+  if (nvo < 0 || !G || !d) return fail("cmpc_qp_solve_batch_map: G and d required for nvo > 0");
+  HIP_TRY(hipSetDevice(device));
+  const size_t q = (size_t)nqp;
+  double* dH; double* dg; double* dG; double* dd; double* dlb; double* dub; double* dlbA; double* dubA; double* dx;
+  uint32_t *dws, *dwo; int32_t *dst, *dnc, *dnt; uint8_t* dtr;
+  HIP_TRY(hipMalloc(&dH, sizeof(double) * q * n * n));
+  HIP_TRY(hipMalloc(&dg, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dG, sizeof(double) * q * n * nvo));
+  HIP_TRY(hipMalloc(&dd, sizeof(double) * q * nvo));
+  HIP_TRY(hipMalloc(&dlb, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dub, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dlbA, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dubA, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dx, sizeof(double) * q * n));
+  HIP_TRY(hipMalloc(&dws, sizeof(uint32_t) * q));
+  HIP_TRY(hipMalloc(&dwo, sizeof(uint32_t) * q));
+  HIP_TRY(hipMalloc(&dst, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dnc, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dnt, sizeof(int32_t) * q));
+  HIP_TRY(hipMalloc(&dtr, 16 * q));
+  HIP_TRY(hipMemcpy(dH, H, sizeof(double) * q * n * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dg, f, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dG, G, sizeof(double) * q * n * nvo, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dd, d, sizeof(double) * q * nvo, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dlb, lb, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dub, ub, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dlbA, lbA, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dubA, ubA, sizeof(double) * q * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dws, ws_in, sizeof(uint32_t) * q, hipMemcpyHostToDevice));
+  QpBatchParams P{dH, dg, dlb, dub, dlbA, dubA, dws, dx, dst, dnc, dnt, dwo, dtr, nqp, max_chg, dG, dd, nvo};
+  if (cmpc_launch_qp_batch_map(P, n, nu, nvo, nullptr)) return fail("map-form qp batch kernel not instantiated");
+  if (check_launch("map-form qp batch kernel")) return -1;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(x, dx, sizeof(double) * q * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nchg, dnc, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ws_out, dwo, sizeof(uint32_t) * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(trace, dtr, 16 * q, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ntrace, dnt, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
+  void* bufs[] = {dH, dg, dG, dd, dlb, dub, dlbA, dubA, dx, dws, dwo, dst, dnc, dnt, dtr};
+  for (void* b : bufs) (void)hipFree(b);
+  return 0;
+}
+
 }  // extern "C"

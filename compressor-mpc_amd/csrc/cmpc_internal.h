@@ -167,7 +167,9 @@ struct BuildParams {
 };
 
 
-// Standalone batched solver (parity / KKT tests).
+// Standalone batched solver (parity / KKT tests).  G (nqp * n * nvo) and d
+// (nqp * nvo) non-null: the Jacobi iteration's map-form solve with g = f + G d
+// (cmpc_qp_solve_batch_map); g is f then.
 struct QpBatchParams {
   const double *H, *g, *lb, *ub, *lbA, *ubA;
   const uint32_t* ws_in;
@@ -176,6 +178,8 @@ struct QpBatchParams {
   uint32_t* ws_out;
   uint8_t* trace;
   int nqp, max_chg;
+  const double *G = nullptr, *d = nullptr;
+  int nvo = 0;
 };
 
 // Device record producer (produce.hip): one scenario's plant linearisation
@@ -296,6 +300,7 @@ int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
 // -1 when not instantiated for these dimensions or S does not divide 4.
 int cmpc_launch_solve_rows(const SolveParams& P, int nV, int nu, int nVo, void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
+int cmpc_launch_qp_batch_map(const QpBatchParams& P, int n, int nu, int nvo, void* stream);
 // Plant simulation (sim.hip)
 struct SimParams {
   double* x;              // B * ns

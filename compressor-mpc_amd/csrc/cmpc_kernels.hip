@@ -745,11 +745,13 @@ template <int N, int NU, int NVO, bool TRACE, bool EXT = false>
 __global__ __launch_bounds__(CMPC_SOLVE_THREADS)
 __attribute__((amdgpu_waves_per_eu(CMPC_SOLVE_WPE(N), CMPC_SOLVE_WPE(N))))
 void cmpc_solve_kernel(SolveParams P) {
-  // nV >= 6 (centralized, m = 3): one wave per SIMD with the AGPR half of the
-  // register file open for spills (an AGPR clobber keeps the compiler from
-  // inferring "no AGPRs"): nV = 8 scratch 1480 -> 464 B per lane, iterate
-  // (K = 1, 65 536 centralized QPs) 0.131 -> 0.049 ms.  nV = 4 stays at two
-  // waves per SIMD (one wave measured 0.073 vs 0.048 ms)
+  // One wave per SIMD with the AGPR half of the register file open for
+  // spills (an AGPR clobber keeps the compiler from inferring "no AGPRs"):
+  // nV = 8 scratch 1480 -> 464 B per lane, iterate (K = 1, 65 536
+  // centralized QPs) 0.131 -> 0.049 ms.  nV = 4 too since the map form (its
+  // map of 40 doubles per lane beside the solver): K = 9 at 131 072 QPs
+  // 32.1 us against 69.6 us at two waves per SIMD with 308 B of spills
+  // (profiles/r5b_small_batch.txt)
   if constexpr (CMPC_SOLVE_WPE(N) == 1) asm volatile("" ::: "a0");
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   const int q_raw = blockIdx.x * blockDim.x + threadIdx.x;
@@ -771,8 +773,16 @@ void cmpc_solve_kernel(SolveParams P) {
     for (int c = 0; c < NVOA; ++c)
       gsh[a * NVOA + c][threadIdx.x] = (NVO > 0) ? rec[N * N + N + a * NVO + c] : 0.0;
 
-  lane_solve_qp<N, NU, NVO, TRACE, EXT, CMPC_SOLVE_THREADS>(P, q, active, s, base_lane, rec,
-                                                           &gsh[0][threadIdx.x]);
+  if constexpr (CMPC_SOLVE_WPE(N) == 2) {
+    // two waves per SIMD: H^-1 (used to build a working set's map and off the
+    // map form's common path) in LDS as well, beside the map in registers
+    __shared__ double hsh[N * N][CMPC_SOLVE_THREADS];
+    lane_solve_qp<N, NU, NVO, TRACE, EXT, CMPC_SOLVE_THREADS, HinvStrided<N, CMPC_SOLVE_THREADS>>(
+        P, q, active, s, base_lane, rec, &gsh[0][threadIdx.x], &hsh[0][threadIdx.x]);
+  } else {
+    lane_solve_qp<N, NU, NVO, TRACE, EXT, CMPC_SOLVE_THREADS>(P, q, active, s, base_lane, rec,
+                                                             &gsh[0][threadIdx.x]);
+  }
 }
 
 // standalone batched solve (parity and KKT tests)
@@ -923,6 +933,66 @@ int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo, void* strea
   SOLVE_CASE(8, 4, 0)   // centralized, m = 2
   SOLVE_CASE(2, 2, 2)   // m = 1
   SOLVE_CASE(6, 2, 6)   // m = 3
+  return -1;
+}
+
+// the map-form solve of one Jacobi iteration (g = f + G d) on standalone
+// QPs: qp_solve_map with a map built for the QP (cmpc_qp_solve_batch_map;
+// DistributedSolver::UpdateAndSolveQP)
+template <int N, int NU, int NVO>
+__global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_map_kernel(QpBatchParams P) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P.nqp) return;
+  double H[N][N], f[N], d[NVO];
+  Qp<N, NU> qp;
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+#pragma unroll
+    for (int b = 0; b < N; ++b) H[a][b] = P.H[(size_t)q * N * N + a * N + b];
+    f[a] = P.g[(size_t)q * N + a];
+    qp.lb[a] = P.lb[(size_t)q * N + a];
+    qp.ub[a] = P.ub[(size_t)q * N + a];
+    qp.lbA[a] = P.lbA[(size_t)q * N + a];
+    qp.ubA[a] = P.ubA[(size_t)q * N + a];
+  }
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) d[c] = P.d[(size_t)q * NVO + c];
+  qp.tolerances();
+  const bool pd = hinv_of<N>(H, qp.Hinv);
+  double hmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) hmax = fabs(H[i][i]) > hmax ? fabs(H[i][i]) : hmax;
+  double xu0[N], U[N][NVO];
+  jmap_terms<N, NVO, 1>(qp.Hinv, f, P.G + (size_t)q * N * NVO, xu0, U);
+  JMap<N, NVO> mp;
+  mp.ws = kWsInvalid;
+  double x[N];
+  QpOut o;
+  qp_solve_map<true, N, NVO>(qp, pd, TOL_D * (1.0 + hmax), xu0, URegs<N, NVO>{U}, d, P.ws_in[q], P.max_chg, x, o,
+                             mp);
+#pragma unroll
+  for (int a = 0; a < N; ++a) P.x[(size_t)q * N + a] = x[a];
+  P.status[q] = o.status;
+  P.nchg[q] = o.nchg;
+  P.ws_out[q] = o.ws;
+  P.ntrace[q] = o.ntrace;
+  uint32_t* tr = reinterpret_cast<uint32_t*>(P.trace + (size_t)q * 16);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) tr[t] = o.tr[t];
+}
+
+int cmpc_launch_qp_batch_map(const QpBatchParams& P, int n, int nu, int nvo, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (P.nqp + CMPC_SOLVE_THREADS - 1) / CMPC_SOLVE_THREADS;
+#define CMPC_QPMAP_CASE(N_, NU_, NVO_)                                                              \
+  if (n == N_ && nu == NU_ && nvo == NVO_) {                                                        \
+    hipLaunchKernelGGL((cmpc_qp_batch_map_kernel<N_, NU_, NVO_>), dim3(grid), dim3(CMPC_SOLVE_THREADS), 0, s, P); \
+    return 0;                                                                                       \
+  }
+  CMPC_QPMAP_CASE(4, 2, 4)
+  CMPC_QPMAP_CASE(6, 2, 6)
+  CMPC_QPMAP_CASE(2, 2, 2)
+#undef CMPC_QPMAP_CASE
   return -1;
 }
 

@@ -8,19 +8,18 @@
 // sub-controller, base_lane = the lane of the scenario's sub-controller 0
 // (the plan exchange reads lanes base_lane + s2 of the same wave).
 #pragma once
+#include <type_traits>
+
 #include "cmpc_internal.h"
 #include "qp_solver.h"
 
-#ifndef CMPC_SOLVE_CACHE
-#define CMPC_SOLVE_CACHE 1  // reuse the working-set factors across Jacobi iterations
-#endif
 #ifndef CMPC_SOLVE_PRIO
 #define CMPC_SOLVE_PRIO 1  // priority by Jacobi-iteration progress (iterate 0.049 -> 0.047 ms)
 #endif
 
-template <int N, int NU, int NVO, bool TRACE, bool EXT, int GSTRIDE>
+template <int N, int NU, int NVO, bool TRACE, bool EXT, int GSTRIDE, class HS = HinvRegs<N>>
 __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool active, int s, int base_lane,
-                                              const double* rec, const double* gb) {
+                                              const double* rec, const double* gb, double* hsh = nullptr) {
   constexpr int M = N / NU;
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
@@ -36,7 +35,9 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
   // bounds repeat every NU entries (rep_m(lower - u_old), rep_m(rate bounds));
   // H^-1 stays in registers (an LDS copy measured slower: the compiler
   // hoists its loads and spills more)
-  Qp<N, NU, NU> qp;
+  // H^-1 in registers, or (HinvStrided) in the caller's LDS column hsh
+  Qp<N, NU, NU, HS> qp;
+  if constexpr (!std::is_same_v<HS, HinvRegs<N>>) qp.Hinv.p = hsh;
   double uo[NU];
 #pragma unroll
   for (int c = 0; c < NU; ++c) uo[c] = P.u_old[(size_t)q * P.nu_tot + c];
@@ -65,12 +66,23 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
   double dprev[N];
 #pragma unroll
   for (int a = 0; a < N; ++a) dprev[a] = P.du_old[(size_t)q * N + a];
-#if CMPC_SOLVE_CACHE
-  // working set + factors of the previous Jacobi iteration's solve (same H):
-  // reused when the working set is unchanged (qp_solve_t, CACHE)
-  WSet<N> wc;
-  uint32_t wc_ws = kWsInvalid;
-#endif
+  // the map form (qp_solver.h): x_u0 = -Hinv f and U = Hinv G once per QP,
+  // the map of the current working set kept across the K iterations
+  // (the iterate kernel, G in its own LDS columns (GSTRIDE > 1): U replaces
+  // G there, the map form reads G only here; the fused steps read G from the
+  // stored QP: U in registers)
+  double xu0[N];
+  constexpr bool UIN = GSTRIDE > 1;
+  double Ur[UIN ? 1 : N][UIN ? 1 : NVOA];
+  if constexpr (UIN) jmap_terms<N, NVO, GSTRIDE>(qp.Hinv, f, const_cast<double*>(gb), xu0);
+  else jmap_terms<N, NVO, GSTRIDE>(qp.Hinv, f, gb, xu0, Ur);
+  using UAcc = std::conditional_t<UIN, UStrided<NVOA, GSTRIDE>, URegs<N, NVOA>>;
+  const UAcc U = [&]() {
+    if constexpr (UIN) return UStrided<NVOA, GSTRIDE>{gb};
+    else return URegs<N, NVOA>{Ur};
+  }();
+  JMap<N, NVO> mp;
+  mp.ws = kWsInvalid;
   for (int k = 0; k < P.K; ++k) {
 #if CMPC_SOLVE_PRIO
     {  // fair progress of the SIMD's waves (cf. build_rows.hip)
@@ -81,11 +93,10 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
       else __builtin_amdgcn_s_setprio(3);
     }
 #endif
-    double fk[N];
+    double dother[NVOA];
 #pragma unroll
-    for (int a = 0; a < N; ++a) fk[a] = f[a];
-    if (NVO > 0 && CMPC_QP_ABL != 3) {
-      double dother[NVOA];
+    for (int c = 0; c < NVOA; ++c) dother[c] = 0.0;
+    if (NVO > 0) {
       if constexpr (EXT) {
         // du_last of DistributedController::GetInput: the other controllers'
         // plans, controller-major, then move, then input (nerve_center.h:283-285)
@@ -120,20 +131,9 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
               dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev[mv * NU + c], base_lane + s2, 64);
         }
       }
-      // f_k = f + (Su_other du_other)' W Su  ==  f + G du_other
-#pragma unroll
-      for (int a = 0; a < N; ++a) {
-        double t = fk[a];
-#pragma unroll
-        for (int c = 0; c < NVOA; ++c) t = t + gb[(a * NVOA + c) * GSTRIDE] * dother[c];
-        fk[a] = t;
-      }
     }
-#if CMPC_SOLVE_CACHE
-    qp_solve_t<TRACE, true>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o, &wc, &wc_ws);
-#else
-    qp_solve_t<TRACE>(qp, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x, o);
-#endif
+    // f_k = f + (Su_other du_other)' W Su = f + G du_other, in the map form
+    qp_solve_map<TRACE, N, NVO>(qp, pd, tol_d, xu0, U, dother, ws, CMPC_NWSR_MAX, x, o, mp);
     ws = o.ws;
 #pragma unroll
     for (int a = 0; a < N; ++a) dprev[a] = x[a];

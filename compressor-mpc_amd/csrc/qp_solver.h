@@ -43,6 +43,17 @@ struct HinvRegs {
   CMPC_HD double operator()(int r, int c) const { return m[r][c]; }
   CMPC_HD void set(int r, int c, double v) { m[r][c] = v; }
 };
+// the upper triangle in a lane-contiguous LDS array (entry (r, c), r <= c,
+// at p[(r * N + c) * STRIDE]), read mirrored: the iterate kernel's map form
+// needs H^-1 only to build a map and off the common path
+template <int N, int STRIDE>
+struct HinvStrided {
+  double* p;
+  CMPC_HD double operator()(int r, int c) const { return r <= c ? p[(r * N + c) * STRIDE] : p[(c * N + r) * STRIDE]; }
+  CMPC_HD void set(int r, int c, double v) {
+    if (r <= c) p[(r * N + c) * STRIDE] = v;
+  }
+};
 
 // NB = stored bound entries: N (general), or NU when the bounds repeat every
 // NU entries (the MPC QP: rep_m(lower - u_old), rep_m(rate bounds),
@@ -53,22 +64,10 @@ struct Qp {
   HS Hinv;
   double lb[NB], ub[NB], lbA[NB], ubA[NB];
   // phase-B violation thresholds -TOL_P (1 + |beta|) per bound and side,
-  // fixed per QP (tolerances() after the bounds are set), so that the K
-  // Jacobi solves of a QP do not recompute them in every scan
-  double tlb[NB], tub[NB], tlbA[NB], tubA[NB];
-  CMPC_HD void tolerances() {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      tlb[i] = -TOL_P * (1.0 + fabs(lb[i]));
-      tub[i] = -TOL_P * (1.0 + fabs(-ub[i]));
-      tlbA[i] = -TOL_P * (1.0 + fabs(lbA[i]));
-      tubA[i] = -TOL_P * (1.0 + fabs(-ubA[i]));
-    }
-  }
-  CMPC_HD double thr(int j, int side) const {
-    if (j < N) return side ? sel<NB>(tub, j % NB) : sel<NB>(tlb, j % NB);
-    return side ? sel<NB>(tubA, (j - N) % NB) : sel<NB>(tlbA, (j - N) % NB);
-  }
+  // formed where they are compared (registers: the iterate kernel's map form
+  // keeps its map beside the bounds)
+  CMPC_HD void tolerances() {}
+  CMPC_HD double thr(int j, int side) const { return -TOL_P * (1.0 + fabs(beta(j, side))); }
   CMPC_HD double lbv(int j) const { return sel<NB>(lb, j % NB); }
   CMPC_HD double ubv(int j) const { return sel<NB>(ub, j % NB); }
 
@@ -133,14 +132,14 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
 // (Qp::normal, the same vector bit for bit), which frees 2 N^2 registers per
 // working set: the centralized nV = 8 solve then needs no scratch.
 #ifndef CMPC_WSET_STORE_MAX
-#define CMPC_WSET_STORE_MAX 6  // largest N whose working sets store their normals
+#define CMPC_WSET_STORE_MAX 0  // largest N whose working sets store their normals and bounds
 #endif
 template <int N, bool SN = (N <= CMPC_WSET_STORE_MAX)>
 struct WSet {
   int K;
   int j[N], side[N];
   double lam[N];
-  double nrm[SN ? N : 1][N], bta[N];
+  double nrm[SN ? N : 1][N], bta[SN ? N : 1];  // normals and bounds (SN) or rebuilt from (j, side)
   double L[N][N], D[N], R[N];
 };
 
@@ -155,11 +154,20 @@ CMPC_HD void wset_normal(const Q& q, const WSet<N, SN>& W, int a, double (&n)[N]
   }
 }
 
+// the bound beta of slot a (stored, or from its constraint index)
+template <int N, bool SN, class Q>
+CMPC_HD double wset_beta(const Q& q, const WSet<N, SN>& W, int a) {
+  if constexpr (SN) return W.bta[a];
+  else return q.beta(W.j[a], W.side[a]);
+}
+
 // LDL' of the leading K x K block of M (lower triangle read) with reciprocal
-// pivots R = 1/D (or_qp.c ldl); returns false on a non-positive pivot.
+// pivots R = 1/D (or_qp.c ldl); returns false unless every pivot
+// d_j > rel * M_jj (rel = 0: H positive definite; TOL_Z: a working set with
+// independent normals).
 template <int N>
 CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D)[N],
-                   double (&R)[N]) {
+                   double (&R)[N], double rel = 0.0) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -167,7 +175,7 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D
       double d = M[j][j];
 #pragma unroll
       for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
-      ok = ok && (d > 0.0);
+      ok = ok && (d > rel * M[j][j]);
       D[j] = d;
       const double r = 1.0 / d;
       R[j] = r;
@@ -251,7 +259,7 @@ CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
       M[b][a] = v;
     }
   }
-  return ldl_k<N>(W.K, M, W.L, W.D, W.R);
+  return ldl_k<N>(W.K, M, W.L, W.D, W.R, TOL_Z);
 }
 
 // remove slot a (or_qp.c wset_remove): the other slots keep their order; the
@@ -297,7 +305,7 @@ CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
       W.j[i] = W.j[i + 1];
       W.side[i] = W.side[i + 1];
       W.lam[i] = W.lam[i + 1];
-      W.bta[i] = W.bta[i + 1];
+      if constexpr (SN) W.bta[i] = W.bta[i + 1];
       W.D[i] = W.D[i + 1];
       W.R[i] = W.R[i + 1];
       if constexpr (SN) {
@@ -322,7 +330,7 @@ CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double 
       W.j[b] = j;
       W.side[b] = side;
       W.lam[b] = lam;
-      W.bta[b] = bta;
+      if constexpr (SN) W.bta[b] = bta;
       if constexpr (SN) {
 #pragma unroll
         for (int c = 0; c < N; ++c) W.nrm[b][c] = n[c];
@@ -377,40 +385,45 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
 
 // TRACE = false: the working-set change trace (QpOut::tr, ntrace) is not
 // recorded (the iterate kernel without CMPC_TRACE); everything else is equal.
-//
-// CACHE = true (the Jacobi loop of the iterate kernel): the caller keeps the
-// working set of the previous solve of the same QP (same H, other g) in *wc,
-// with *wc_ws its working-set word, or kWsInvalid.  When ws_in equals it, the
-// warm start takes the slots and the LDL' factor of M = N' H^-1 N from *wc
-// instead of rebuilding them: the same values (the warm start's slot order
-// and full factor are a deterministic function of H and the working set), so
-// the result and the trace are bit-identical to the uncached solve.  *wc_ws
-// is set only after a solve that ends OK without a working-set change (an
-// update-derived factor, or slots in append order, would differ in rounding
-// from the warm start's fresh factor).
 constexpr uint32_t kWsInvalid = 0xFFFFFFFFu;
 
-template <bool TRACE, bool CACHE = false, int N, int NU, int NB, class HS>
+// the warm start's slots: the constraints of ws_in in ascending j
+template <int N, bool SN, class Q>
+CMPC_HD void wset_fill(const Q& q, uint32_t ws_in, WSet<N, SN>& W) {
+  W.K = 0;
+  uint32_t msk = ws_in & ((1u << (2 * N)) - 1u);
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    W.j[a] = 0;
+    W.side[a] = 0;
+    W.lam[a] = 0.0;
+    if (msk) {
+      const int j = __builtin_ctz(msk);
+      msk &= msk - 1u;
+      const int sd = (ws_in >> (16 + j)) & 1u;
+      W.j[a] = j;
+      W.side[a] = sd;
+      if constexpr (SN) q.normal(j, sd, W.nrm[a]);
+      if constexpr (SN) W.bta[a] = q.beta(j, sd);
+      W.K = a + 1;
+    }
+  }
+}
+
+template <bool TRACE, int N, int NU, int NB, class HS, bool SN>
+CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[N], int chg, bool done,
+                        int max_chg, QpOut& o);
+
+// The plain solve (standalone QPs, InitializeQPProblem, the coupled
+// iteration): g given, the map form with nvo = 0 (or_qp.c).
+template <bool TRACE, int N, int NU, int NB, class HS>
 CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],
-                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o,
-                         WSet<N>* wc = nullptr, uint32_t* wc_ws = nullptr) {
-  WSet<N> Wl;
-  WSet<N>& W = CACHE ? *wc : Wl;
-  constexpr bool SN = (N <= CMPC_WSET_STORE_MAX);
-  const bool cached = CACHE && pd && *wc_ws == ws_in;
+                         uint32_t ws_in, int max_chg, double (&x)[N], QpOut& o) {
+  WSet<N> W;
   o.status = CMPC_QP_OK;
   o.nchg = 0;
   o.ntrace = 0;
   o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
-  if (!cached) {
-    W.K = 0;
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-      W.j[a] = 0;
-      W.side[a] = 0;
-      W.lam[a] = 0.0;
-    }
-  }
   int chg = 0;
   bool done = false;
   double xu[N];
@@ -427,26 +440,10 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   }
   // A. warm start: slot a = the a-th active constraint of ws_in in ascending
   // j (the oracle adds them in that order while K < n), then the full factor
-  if (!cached) {
-    uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-      if (msk) {
-        const int j = __builtin_ctz(msk);
-        msk &= msk - 1u;
-        const int sd = (ws_in >> (16 + j)) & 1u;
-        W.j[a] = j;
-        W.side[a] = sd;
-        W.lam[a] = 0.0;
-        if constexpr (SN) q.normal(j, sd, W.nrm[a]);
-        W.bta[a] = q.beta(j, sd);
-        W.K = a + 1;
-      }
-    }
-    if (W.K > 0 && !wset_factor<N>(q, W)) {  // inconsistent warm start: cold
-      W.K = 0;
-      ++chg;
-    }
+  wset_fill(q, done ? 0u : ws_in, W);
+  if (W.K > 0 && !wset_factor<N>(q, W)) {  // inconsistent warm start: cold
+    W.K = 0;
+    ++chg;
   }
   for (int it = 0; it <= N && !done; ++it) {
     double rhs[N];
@@ -456,7 +453,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       if (a < W.K) {
         double na[N];
         wset_normal(q, W, a, na);
-        rhs[a] = W.bta[a] - ndot<N>(na, xu);
+        rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu);
       }
     }
     ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
@@ -499,6 +496,14 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       }
     }
   }
+  qp_phase_b<TRACE>(q, W, x, chg, done, max_chg, o);
+}
+
+// Phase B (Goldfarb–Idnani) from the phase-A point x and multipliers W.lam,
+// then the result: working-set word, finite check, bound fixing / zero move.
+template <bool TRACE, int N, int NU, int NB, class HS, bool SN>
+CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[N], int chg, bool done,
+                        int max_chg, QpOut& o) {
   // B. Goldfarb–Idnani
   for (int outer = 0; outer <= max_chg + 1 && !done && CMPC_QP_ABL != 1; ++outer) {
     int pj = -1, ps = 0;
@@ -535,13 +540,15 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       }
     }
     if (pj < 0) break;  // optimal
-    double np_[N];
-    q.normal(pj, ps, np_);
     const double bp = q.beta(pj, ps);
     double up = 0.0;
     for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
       double hp[N], qv[N], rv[N], zz[N], z[N];
-      q.hinv_n(np_, hp);
+      {
+        double np_[N];  // (rebuilt here: registers)
+        q.normal(pj, ps, np_);
+        q.hinv_n(np_, hp);
+      }
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         qv[a] = 0.0;
@@ -564,8 +571,8 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
           for (int r = 0; r < N; ++r) z[r] = z[r] - rv[a] * ha[r];
         }
       }
-      const double zn = ndot<N>(np_, z);
-      const double den = ndot<N>(np_, hp);
+      const double zn = q.nu_dot(pj, ps, z);
+      const double den = q.nu_dot(pj, ps, hp);
       int k = -1;
       double t1 = 0.0;
 #pragma unroll
@@ -577,7 +584,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
             k = a;
           }
         }
-      if (zn <= TOL_Z * den) {
+      if (zn <= TOL_Z * den || W.K >= N) {  // dependent (n active: always)
         if (k < 0) {
           o.status = CMPC_QP_INFEASIBLE;
           done = true;
@@ -604,7 +611,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         continue;
       }
       const double rzn = 1.0 / zn;
-      const double sl = ndot<N>(np_, x) - bp;
+      const double sl = q.nu_dot(pj, ps, x) - bp;
       const double t2 = -sl * rzn;
       const bool full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
@@ -616,6 +623,8 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
       up = up + t;
       if (full) {
         if (TRACE) trace_push(o, 1, pj, ps);
+        double np_[N];
+        if constexpr (SN) q.normal(pj, ps, np_);
         wset_add<N>(W, pj, ps, up, np_, bp, zz, zn, rzn);
         if (++chg > max_chg) {
           o.status = CMPC_QP_MAX_NWSR;
@@ -645,10 +654,8 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   for (int a = 0; a < N; ++a)
     if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
   o.ws = w;
-  if (CACHE) *wc_ws = (o.status == CMPC_QP_OK && chg == 0) ? w : kWsInvalid;
   // a non-finite plan (a NaN or infinite gradient) fails like any other
-  // non-success: zero move (or_qp.c; checked before the bound fixing).  The
-  // cached factors stay valid: they depend on H and the working set only.
+  // non-success: zero move (or_qp.c; checked before the bound fixing)
   if (o.status == CMPC_QP_OK) {
     bool fin = true;
 #pragma unroll
@@ -670,6 +677,331 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   }
 }
 
+// ---------------------------------------------------------------------------
+// Map form of the Jacobi iterations (or_qp.c step A, version 3).  Within one
+// control step a QP keeps H, f and G = Su'W Su_other; only the other
+// sub-controllers' plans d change between its K solves.  For a working set W
+// the multipliers and the point are affine in d:
+//   lam = lam0 + Lam d,  x = x0 + X d  (x_u0 = -Hinv f, U = Hinv G,
+//   lam0 = M^-1 (beta_W - N' x_u0), Lam = M^-1 N' U, x0 = x_u0 + H_W lam0,
+//   X = -U + H_W Lam),
+// so an iteration whose working set is the one of the map costs two small
+// products.  The map is a deterministic function of (H, f, G, bounds, W):
+// JMap keeps the last one built (ws = its working-set word) across the
+// iterations, and a rebuilt map equals a kept one bit for bit.
+// ---------------------------------------------------------------------------
+template <int N, int NVO>
+struct JMap {
+  static constexpr int NVOA = NVO > 0 ? NVO : 1;
+  uint32_t ws;   // the ws_in the map was built for, kWsInvalid: none
+  uint32_t wc;   // the working-set word of its slots
+  int K;         // its slot count
+  double lam0[N], Lam[N][NVOA], x0[N], X[N][NVOA];
+};
+
+// U = Hinv G in registers, or in the lane's column of an LDS array
+// (element (r, c) at p[(r * NVOA + c) * STRIDE])
+template <int N, int NVOA>
+struct URegs {
+  const double (&U)[N][NVOA];
+  CMPC_HD double operator()(int r, int c) const { return U[r][c]; }
+};
+template <int NVOA, int STRIDE>
+struct UStrided {
+  const double* p;
+  CMPC_HD double operator()(int r, int c) const { return p[(r * NVOA + c) * STRIDE]; }
+};
+
+// the map of the WSet's slots (fresh warm-start factor)
+template <int N, int NVO, int NU, int NB, class HS, bool SN, class UA>
+CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const double (&xu0)[N],
+                        const UA& U, JMap<N, NVO>& mp) {
+  double rhs[N];
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    rhs[a] = 0.0;
+    if (a < W.K) {
+      double na[N];
+      wset_normal(q, W, a, na);
+      rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu0);
+    }
+  }
+  ldl_solve_k<N>(W.K, W.L, W.R, rhs, mp.lam0);
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) {
+    double uc[N], lc[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) uc[r] = U(r, c);
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      rhs[a] = 0.0;
+      if (a < W.K) {
+        double na[N];
+        wset_normal(q, W, a, na);
+        rhs[a] = ndot<N>(na, uc);
+      }
+    }
+    ldl_solve_k<N>(W.K, W.L, W.R, rhs, lc);
+#pragma unroll
+    for (int a = 0; a < N; ++a) mp.Lam[a][c] = lc[a];  // zero from K on
+  }
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    mp.x0[r] = xu0[r];
+#pragma unroll
+    for (int c = 0; c < NVO; ++c) mp.X[r][c] = -U(r, c);
+  }
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    if (a < W.K) {
+      double na[N], ha[N];
+      wset_normal(q, W, a, na);
+      q.hinv_n(na, ha);
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        mp.x0[r] = mp.x0[r] + mp.lam0[a] * ha[r];
+#pragma unroll
+        for (int c = 0; c < NVO; ++c) mp.X[r][c] = mp.X[r][c] + mp.Lam[a][c] * ha[r];
+      }
+    }
+  }
+}
+
+// the working-set word of the first K slots
+template <int N, bool SN>
+CMPC_HD uint32_t wset_word(const WSet<N, SN>& W) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+    if (a < W.K) w |= (1u << W.j[a]) | ((uint32_t)W.side[a] << (16 + W.j[a]));
+  return w;
+}
+
+// One Jacobi-iteration solve in the map form: xu0 = -Hinv f and U = Hinv G
+// of the step's QP, d the other plans; mp persists across the QP's
+// iterations (mp.ws = kWsInvalid before the first).  A solve on the map's
+// working set that stays on it (no multiplier below -tol_d, no violated
+// constraint) touches only the map; otherwise the working set and its fresh
+// factor are rebuilt from ws_in (the same values as when the map was built)
+// and the solve continues as the plain one.
+template <bool TRACE, int N, int NVO, int NU, int NB, class HS, class UA>
+CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&xu0)[N],
+                          const UA& U, const double (&d)[JMap<N, NVO>::NVOA], uint32_t ws_in, int max_chg,
+                          double (&x)[N], QpOut& o, JMap<N, NVO>& mp) {
+  WSet<N> W;
+  o.status = CMPC_QP_OK;
+  o.nchg = 0;
+  o.ntrace = 0;
+  o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
+  int chg = 0;
+  bool done = false, have_w = false;
+  if (!pd) {
+    o.status = CMPC_QP_NOT_PD;
+    done = true;
+    W.K = 0;
+    have_w = true;
+    mp.ws = kWsInvalid;
+  } else if (ws_in != mp.ws) {
+    // the warm start (slots, full factor) and its map
+    wset_fill(q, ws_in, W);
+    if (W.K > 0 && !wset_factor<N>(q, W)) {  // inconsistent warm start: cold
+      W.K = 0;
+      ++chg;
+    }
+    have_w = true;
+    jmap_build<N, NVO>(q, W, xu0, U, mp);
+    mp.K = W.K;
+    mp.wc = wset_word(W);
+    mp.ws = chg ? kWsInvalid : ws_in;  // (a failed warm start is redone)
+  }
+  // A. lam = lam0 + Lam d (entries from K on are zero)
+  double lam[N];
+  int worst = -1;
+  {
+    double wv = -tol_d;
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      double v = mp.lam0[a];
+#pragma unroll
+      for (int c = 0; c < NVO; ++c) v = v + mp.Lam[a][c] * d[c];
+      lam[a] = v;
+      if (a < mp.K && v < wv) {
+        wv = v;
+        worst = a;
+      }
+    }
+  }
+  if (done) worst = -1;
+  bool stay = !done && worst < 0;
+  if (stay) {
+    // x = x0 + X d, then the phase-B scan: nothing violated -> done here
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double v = mp.x0[r];
+#pragma unroll
+      for (int c = 0; c < NVO; ++c) v = v + mp.X[r][c] * d[c];
+      x[r] = v;
+    }
+    bool anyv = false;
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j)
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        anyv = anyv | (!((mp.wc >> j) & 1u) && (q.nu_dot(j, sd, x) - q.beta(j, sd) < q.thr(j, sd)));
+    if (!anyv && CMPC_QP_ABL != 1) {
+      o.nchg = chg;
+      o.ws = mp.wc;
+      bool fin = true;
+#pragma unroll
+      for (int r = 0; r < N; ++r) fin = fin && __builtin_isfinite(x[r]);
+      if (!fin) o.status = CMPC_QP_NONFINITE;
+      if (o.status == CMPC_QP_OK) {
+        const uint32_t bnd = mp.wc & ((1u << N) - 1u), up = (mp.wc >> 16) & bnd;
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+          x[r] = ((bnd >> r) & 1u) ? (((up >> r) & 1u) ? q.ubv(r) : q.lbv(r)) : x[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < N; ++r) x[r] = 0.0;
+      }
+      return;
+    }
+  }
+  // off the map: the map is dropped (its registers are free for the slow
+  // path; after a working-set change the next ws_in is another anyway), and
+  // the working set of ws_in is rebuilt with its fresh factor
+  mp.ws = kWsInvalid;
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    mp.lam0[a] = 0.0;
+    mp.x0[a] = 0.0;
+#pragma unroll
+    for (int c = 0; c < JMap<N, NVO>::NVOA; ++c) {
+      mp.Lam[a][c] = 0.0;
+      mp.X[a][c] = 0.0;
+    }
+  }
+  if (!have_w) {
+    wset_fill(q, ws_in, W);
+    wset_factor<N>(q, W);  // (succeeded when the map was built)
+  }
+#pragma unroll
+  for (int a = 0; a < N; ++a) W.lam[a] = lam[a];
+  if (!done && !stay) {
+    // leave the map: x_u = x_u0 - U d, drops by the factor removal
+    double xu[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double v = xu0[r];
+#pragma unroll
+      for (int c = 0; c < NVO; ++c) v = v - U(r, c) * d[c];
+      xu[r] = v;
+    }
+    for (int it = 0; it <= N && !done; ++it) {
+      if (it > 0) {
+        double rhs[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          rhs[a] = 0.0;
+          if (a < W.K) {
+            double na[N];
+            wset_normal(q, W, a, na);
+            rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu);
+          }
+        }
+        ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
+        worst = -1;
+        double wv = -tol_d;
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          if (a < W.K && W.lam[a] < wv) {
+            wv = W.lam[a];
+            worst = a;
+          }
+      }
+      if (worst < 0) break;
+      int wj = 0, wsd = 0;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a == worst) {
+          wj = W.j[a];
+          wsd = W.side[a];
+        }
+      if (TRACE) trace_push(o, 0, wj, wsd);
+      wset_drop<N>(W, worst);
+      if (++chg > max_chg) {
+        o.status = CMPC_QP_MAX_NWSR;
+        done = true;
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int r = 0; r < N; ++r) x[r] = xu[r];
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        if (a < W.K) {
+          double na[N], ha[N];
+          wset_normal(q, W, a, na);
+          q.hinv_n(na, ha);
+#pragma unroll
+          for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
+        }
+      }
+    }
+  }
+  qp_phase_b<TRACE>(q, W, x, chg, done, max_chg, o);
+}
+
+// x_u0 = -Hinv f and U = Hinv G of a QP (the map form's per-step terms):
+// G[a][c] = gb[(a * NVOA + c) * GSTRIDE], overwritten by U (column c of U
+// once column c of G is read)
+template <int N, int NVO, int GSTRIDE, class HS>
+CMPC_HD void jmap_terms(const HS& Hinv, const double (&f)[N], double* gb, double (&xu0)[N]) {
+  constexpr int NVOA = JMap<N, NVO>::NVOA;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sacc = sacc + Hinv(i, j) * f[j];
+    xu0[i] = -sacc;
+  }
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) {
+    double gc[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) gc[j] = gb[(j * NVOA + c) * GSTRIDE];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double u = 0.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) u = u + Hinv(i, j) * gc[j];
+      gb[(i * NVOA + c) * GSTRIDE] = u;
+    }
+  }
+}
+
+// the same with U in registers (G left in place)
+template <int N, int NVO, int GSTRIDE, class HS>
+CMPC_HD void jmap_terms(const HS& Hinv, const double (&f)[N], const double* gb, double (&xu0)[N],
+                        double (&U)[N][JMap<N, NVO>::NVOA]) {
+  constexpr int NVOA = JMap<N, NVO>::NVOA;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sacc = sacc + Hinv(i, j) * f[j];
+    xu0[i] = -sacc;
+#pragma unroll
+    for (int c = 0; c < NVOA; ++c) {
+      double u = 0.0;
+      if (c < NVO) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) u = u + Hinv(i, j) * gb[(j * NVOA + c) * GSTRIDE];
+      }
+      U[i][c] = u;
+    }
+  }
+}
 
 template <int N, int NU, int NB, class HS>
 CMPC_HD void qp_solve(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&g)[N],

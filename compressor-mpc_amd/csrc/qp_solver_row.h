@@ -1,6 +1,6 @@
 // Row-parallel form of the QP solver (qp_solver.h) for batches too small to
 // fill the GPU with one QP per lane: one QP per 16-lane DPP row, four per
-// wave64.  Same specification (oracle/or_qp.c, version 2) and arithmetic
+// wave64.  Same specification (oracle/or_qp.c, version 3) and arithmetic
 // order as qp_solve_t, bit for bit:
 //  - vectors stay distributed: lane l < N holds row l of H^-1 (registers and
 //    this QP's N x N LDS scratch T), and entry l of x_u, x, H^-1 nu_p, z;
@@ -165,9 +165,10 @@ __device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowb
   for (int j = 0; j < N; ++j) {
     if (j < W.K) {
       double d = nval<N, NU>(hv[j], rowbase, W.j[j], W.side[j]);
+      const double mjj = d;
 #pragma unroll
       for (int k = 0; k < j; ++k) d = d - (W.L[j][k] * W.L[j][k]) * W.D[k];
-      ok = ok && (d > 0.0);
+      ok = ok && (d > TOL_Z * mjj);
       W.D[j] = d;
       const double r = 1.0 / d;
       W.R[j] = r;
@@ -240,98 +241,12 @@ __device__ __forceinline__ int row_scan(double x_l, const RowScan& sc, uint32_t 
   return pj;
 }
 
-// qp_solve_t<TRACE, CACHE = false> for the QP of this row: g_l = entry l of
-// the gradient, t = hinv_row's LDS scratch, hr = row l of H^-1, sc the scan
-// constants; x_l = entry l of the solution (zero on failure).
+// Phase B (Goldfarb–Idnani) of the row's QP from the phase-A point x_l and
+// multipliers W.lam, then the result (qp_phase_b).
 template <bool TRACE, int N, int NU>
-__device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double (&hr)[N], const double* t,
-                                             const RowScan& sc, int l, bool pd, double tol_d, double g_l,
-                                             uint32_t ws_in, int max_chg, double& x_l, QpOut& o) {
-  const int rowbase = (int)(__lane_id() & ~15u);
-  WSet<N, false> W;
-  o.status = CMPC_QP_OK;
-  o.nchg = 0;
-  o.ntrace = 0;
-  o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
-  W.K = 0;
-#pragma unroll
-  for (int a = 0; a < N; ++a) {
-    W.j[a] = 0;
-    W.side[a] = 0;
-    W.lam[a] = 0.0;
-  }
-  int chg = 0;
-  bool done = false;
-  if (!pd) {
-    o.status = CMPC_QP_NOT_PD;
-    done = true;
-  }
-  double xu_l;
-  {
-    double G[N];
-    row_gather<N>(g_l, G);
-    double sacc = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * G[j];
-    xu_l = -sacc;
-  }
-  // A. warm start: slots in ascending j, the full factor
-  {
-    uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-      if (msk) {
-        const int j = __builtin_ctz(msk);
-        msk &= msk - 1u;
-        const int sd = (ws_in >> (16 + j)) & 1u;
-        W.j[a] = j;
-        W.side[a] = sd;
-        W.lam[a] = 0.0;
-        W.bta[a] = q.beta(j, sd);
-        W.K = a + 1;
-      }
-    }
-    if (W.K > 0 && !wset_factor_row<N, NU>(t, l, rowbase, W)) {  // inconsistent warm start: cold
-      W.K = 0;
-      ++chg;
-    }
-  }
-  for (int it = 0; it <= N && !done; ++it) {
-    double rhs[N];
-#pragma unroll
-    for (int a = 0; a < N; ++a) rhs[a] = (a < W.K) ? W.bta[a] - nval<N, NU>(xu_l, rowbase, W.j[a], W.side[a]) : 0.0;
-    ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
-    int worst = -1;
-    double wv = -tol_d;
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-      if (a < W.K && W.lam[a] < wv) {
-        wv = W.lam[a];
-        worst = a;
-      }
-    if (worst < 0) break;
-    int wj = 0, wsd = 0;
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-      if (a == worst) {
-        wj = W.j[a];
-        wsd = W.side[a];
-      }
-    if (TRACE) trace_push(o, 0, wj, wsd);
-    wset_drop<N>(W, worst);
-    if (++chg > max_chg) {
-      o.status = CMPC_QP_MAX_NWSR;
-      done = true;
-    }
-  }
-  x_l = 0.0;
-  if (!done) {
-    // x = xu + sum_a lam_a h_a (entry l, a ascending)
-    x_l = xu_l;
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-      if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
-  }
+__device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const double* t, const RowScan& sc,
+                                               int l, int rowbase, WSet<N, false>& W, double& x_l, int chg,
+                                               bool done, int max_chg, QpOut& o) {
   // B. Goldfarb–Idnani
   for (int outer = 0; outer <= max_chg + 1 && !done; ++outer) {
     uint32_t act = 0;
@@ -366,7 +281,7 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
             k = a;
           }
         }
-      if (zn <= TOL_Z * den) {
+      if (zn <= TOL_Z * den || W.K >= N) {  // dependent (n active: always)
         if (k < 0) {
           o.status = CMPC_QP_INFEASIBLE;
           done = true;
@@ -443,4 +358,290 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
   } else {
     x_l = 0.0;
   }
+}
+
+
+// qp_solve_t for the QP of this row: g_l = entry l of
+// the gradient, t = hinv_row's LDS scratch, hr = row l of H^-1, sc the scan
+// constants; x_l = entry l of the solution (zero on failure).
+template <bool TRACE, int N, int NU>
+__device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double (&hr)[N], const double* t,
+                                             const RowScan& sc, int l, bool pd, double tol_d, double g_l,
+                                             uint32_t ws_in, int max_chg, double& x_l, QpOut& o) {
+  const int rowbase = (int)(__lane_id() & ~15u);
+  WSet<N, false> W;
+  o.status = CMPC_QP_OK;
+  o.nchg = 0;
+  o.ntrace = 0;
+  o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
+  W.K = 0;
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    W.j[a] = 0;
+    W.side[a] = 0;
+    W.lam[a] = 0.0;
+  }
+  int chg = 0;
+  bool done = false;
+  if (!pd) {
+    o.status = CMPC_QP_NOT_PD;
+    done = true;
+  }
+  double xu_l;
+  {
+    double G[N];
+    row_gather<N>(g_l, G);
+    double sacc = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * G[j];
+    xu_l = -sacc;
+  }
+  // A. warm start: slots in ascending j, the full factor
+  {
+    uint32_t msk = done ? 0u : (ws_in & ((1u << (2 * N)) - 1u));
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      if (msk) {
+        const int j = __builtin_ctz(msk);
+        msk &= msk - 1u;
+        const int sd = (ws_in >> (16 + j)) & 1u;
+        W.j[a] = j;
+        W.side[a] = sd;
+        W.lam[a] = 0.0;
+        W.K = a + 1;
+      }
+    }
+    if (W.K > 0 && !wset_factor_row<N, NU>(t, l, rowbase, W)) {  // inconsistent warm start: cold
+      W.K = 0;
+      ++chg;
+    }
+  }
+  for (int it = 0; it <= N && !done; ++it) {
+    double rhs[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) rhs[a] = (a < W.K) ? wset_beta(q, W, a) - nval<N, NU>(xu_l, rowbase, W.j[a], W.side[a]) : 0.0;
+    ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
+    int worst = -1;
+    double wv = -tol_d;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a < W.K && W.lam[a] < wv) {
+        wv = W.lam[a];
+        worst = a;
+      }
+    if (worst < 0) break;
+    int wj = 0, wsd = 0;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a == worst) {
+        wj = W.j[a];
+        wsd = W.side[a];
+      }
+    if (TRACE) trace_push(o, 0, wj, wsd);
+    wset_drop<N>(W, worst);
+    if (++chg > max_chg) {
+      o.status = CMPC_QP_MAX_NWSR;
+      done = true;
+    }
+  }
+  x_l = 0.0;
+  if (!done) {
+    // x = xu + sum_a lam_a h_a (entry l, a ascending)
+    x_l = xu_l;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+      if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+  }
+  qp_row_phase_b<TRACE, N, NU>(q, t, sc, l, rowbase, W, x_l, chg, done, max_chg, o);
+}
+
+// The map form of the Jacobi iterations (qp_solve_map) for the row's QP:
+// lam0, Lam replicated, x0 and X distributed (entry / row l in lane l).
+template <int N, int NVO>
+struct RowMap {
+  static constexpr int NVOA = NVO > 0 ? NVO : 1;
+  uint32_t ws, wc;
+  int K;
+  double lam0[N], Lam[N][NVOA];
+  double x0_l, X_l[NVOA];
+};
+
+// x_u0 = -Hinv f and U = Hinv G, entry / row l (jmap_terms): f_l, Gl = row l
+// of G
+template <int N, int NVO>
+__device__ __forceinline__ void row_jmap_terms(const double (&hr)[N], double f_l,
+                                               const double (&Gl)[RowMap<N, NVO>::NVOA], double& xu0_l,
+                                               double (&U_l)[RowMap<N, NVO>::NVOA]) {
+  double F[N];
+  row_gather<N>(f_l, F);
+  double sacc = 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * F[j];
+  xu0_l = -sacc;
+#pragma unroll
+  for (int c = 0; c < RowMap<N, NVO>::NVOA; ++c) U_l[c] = 0.0;
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) {
+    double Gc[N];
+    row_gather<N>(Gl[c], Gc);
+    double u = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) u = u + hr[j] * Gc[j];
+    U_l[c] = u;
+  }
+}
+
+template <int N, int NU, int NVO>
+__device__ __forceinline__ void row_jmap_build(const RowQp<N, NU>& q, const double* t, int l, int rowbase,
+                                               const WSet<N, false>& W,
+                                               double xu0_l, const double (&U_l)[RowMap<N, NVO>::NVOA],
+                                               RowMap<N, NVO>& mp) {
+  double rhs[N];
+#pragma unroll
+  for (int a = 0; a < N; ++a) rhs[a] = (a < W.K) ? wset_beta(q, W, a) - nval<N, NU>(xu0_l, rowbase, W.j[a], W.side[a]) : 0.0;
+  ldl_solve_k<N>(W.K, W.L, W.R, rhs, mp.lam0);
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) {
+    double lc[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) rhs[a] = (a < W.K) ? nval<N, NU>(U_l[c], rowbase, W.j[a], W.side[a]) : 0.0;
+    ldl_solve_k<N>(W.K, W.L, W.R, rhs, lc);
+#pragma unroll
+    for (int a = 0; a < N; ++a) mp.Lam[a][c] = lc[a];
+  }
+  mp.x0_l = xu0_l;
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) mp.X_l[c] = -U_l[c];
+#pragma unroll
+  for (int a = 0; a < N; ++a) {
+    if (a < W.K) {
+      const double h = hval<N, NU>(t, l, W.j[a], W.side[a]);
+      mp.x0_l = mp.x0_l + mp.lam0[a] * h;
+#pragma unroll
+      for (int c = 0; c < NVO; ++c) mp.X_l[c] = mp.X_l[c] + mp.Lam[a][c] * h;
+    }
+  }
+}
+
+// qp_solve_map for the row's QP (xu0_l, U_l from row_jmap_terms; d the
+// other plans, replicated); mp persists across the QP's iterations
+template <bool TRACE, int N, int NU, int NVO>
+__device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const double* t, const RowScan& sc, int l,
+                                                 bool pd, double tol_d, double xu0_l,
+                                                 const double (&U_l)[RowMap<N, NVO>::NVOA],
+                                                 const double (&d)[RowMap<N, NVO>::NVOA], uint32_t ws_in,
+                                                 int max_chg, double& x_l, QpOut& o, RowMap<N, NVO>& mp) {
+  const int rowbase = (int)(__lane_id() & ~15u);
+  WSet<N, false> W;
+  o.status = CMPC_QP_OK;
+  o.nchg = 0;
+  o.ntrace = 0;
+  o.tr[0] = o.tr[1] = o.tr[2] = o.tr[3] = 0xFFFFFFFFu;
+  int chg = 0;
+  bool done = false, have_w = false;
+  if (!pd) {
+    o.status = CMPC_QP_NOT_PD;
+    done = true;
+    W.K = 0;
+    have_w = true;
+    mp.ws = kWsInvalid;
+  } else if (ws_in != mp.ws) {
+    wset_fill(q, ws_in, W);
+    if (W.K > 0 && !wset_factor_row<N, NU>(t, l, rowbase, W)) {  // inconsistent warm start: cold
+      W.K = 0;
+      ++chg;
+    }
+    have_w = true;
+    row_jmap_build<N, NU, NVO>(q, t, l, rowbase, W, xu0_l, U_l, mp);
+    mp.K = W.K;
+    mp.wc = wset_word(W);
+    mp.ws = chg ? kWsInvalid : ws_in;
+  }
+  double lam[N];
+  int worst = -1;
+  {
+    double wv = -tol_d;
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      double v = mp.lam0[a];
+#pragma unroll
+      for (int c = 0; c < NVO; ++c) v = v + mp.Lam[a][c] * d[c];
+      lam[a] = v;
+      if (a < mp.K && v < wv) {
+        wv = v;
+        worst = a;
+      }
+    }
+  }
+  if (done) worst = -1;
+  const bool stay = !done && worst < 0;
+  x_l = 0.0;
+  if (stay) {
+    double v = mp.x0_l;
+#pragma unroll
+    for (int c = 0; c < NVO; ++c) v = v + mp.X_l[c] * d[c];
+    x_l = v;
+    int ps = 0;
+    if (row_scan<N, NU>(x_l, sc, mp.wc, l, rowbase, ps) < 0) {  // nothing violated: done
+      o.nchg = chg;
+      o.ws = mp.wc;
+      const unsigned long long bad = __ballot(l < N && !__builtin_isfinite(x_l));
+      if ((bad >> rowbase) & 0xFFFFull) o.status = CMPC_QP_NONFINITE;
+      if (o.status == CMPC_QP_OK) {
+        if (l < N && ((mp.wc >> l) & 1u)) x_l = ((mp.wc >> (16 + l)) & 1u) ? q.ubv(l) : q.lbv(l);
+      } else {
+        x_l = 0.0;
+      }
+      return;
+    }
+  }
+  if (!have_w) {
+    wset_fill(q, ws_in, W);
+    wset_factor_row<N, NU>(t, l, rowbase, W);  // (succeeded when the map was built)
+  }
+#pragma unroll
+  for (int a = 0; a < N; ++a) W.lam[a] = lam[a];
+  if (!done && !stay) {
+    double xu_l = xu0_l;
+#pragma unroll
+    for (int c = 0; c < NVO; ++c) xu_l = xu_l - U_l[c] * d[c];
+    for (int it = 0; it <= N && !done; ++it) {
+      if (it > 0) {
+        double rhs[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          rhs[a] = (a < W.K) ? wset_beta(q, W, a) - nval<N, NU>(xu_l, rowbase, W.j[a], W.side[a]) : 0.0;
+        ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
+        worst = -1;
+        double wv = -tol_d;
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+          if (a < W.K && W.lam[a] < wv) {
+            wv = W.lam[a];
+            worst = a;
+          }
+      }
+      if (worst < 0) break;
+      int wj = 0, wsd = 0;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a == worst) {
+          wj = W.j[a];
+          wsd = W.side[a];
+        }
+      if (TRACE) trace_push(o, 0, wj, wsd);
+      wset_drop<N>(W, worst);
+      if (++chg > max_chg) {
+        o.status = CMPC_QP_MAX_NWSR;
+        done = true;
+      }
+    }
+    if (!done) {
+      x_l = xu_l;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+        if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+    }
+  }
+  qp_row_phase_b<TRACE, N, NU>(q, t, sc, l, rowbase, W, x_l, chg, done, max_chg, o);
 }

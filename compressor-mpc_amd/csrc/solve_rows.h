@@ -67,6 +67,12 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
   if constexpr (NVO == 0) {
     if (own) dprev_l = P.du_old[(size_t)q * N + l];
   }
+  // the map form (qp_solver_row.h): x_u0 and U = Hinv G once per QP, the map
+  // of the current working set kept across the K iterations
+  double xu0_l, U_l[NVOA];
+  row_jmap_terms<N, NVO>(hr, f_l, Gl, xu0_l, U_l);
+  RowMap<N, NVO> mp;
+  mp.ws = kWsInvalid;
   for (int k = 0; k < P.K; ++k) {
     {  // fair progress of the SIMD's waves (cf. cmpc_solve_kernel)
       const int level = 3 - (4 * k) / (P.K > 0 ? P.K : 1);
@@ -75,9 +81,10 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
       else if (level == 2) __builtin_amdgcn_s_setprio(2);
       else __builtin_amdgcn_s_setprio(3);
     }
-    double fk = f_l;
+    double dother[NVOA];
+#pragma unroll
+    for (int c = 0; c < NVOA; ++c) dother[c] = 0.0;
     if constexpr (NVO > 0) {
-      double dother[NVOA];
       if constexpr (EXT) {
         // du_last of DistributedController::GetInput (nerve_center.h:283-285)
 #pragma unroll
@@ -100,11 +107,10 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
               dother[mv * (SM1 * NU) + rk * NU + c] = __shfl(dprev_l, base_lane + 16 * s2 + mv * NU + c, 64);
         }
       }
-      // f_k = f + G du_other, entry l (cmpc_solve_kernel's order)
-#pragma unroll
-      for (int c = 0; c < NVOA; ++c) fk = fk + Gl[c] * dother[c];
     }
-    qp_solve_row<TRACE, N, NU>(qp, hr, tsh, sc, l, pd, tol_d, fk, ws, CMPC_NWSR_MAX, x_l, o);
+    // f_k = f + G du_other, in the map form
+    qp_solve_row_map<TRACE, N, NU, NVO>(qp, tsh, sc, l, pd, tol_d, xu0_l, U_l, dother, ws, CMPC_NWSR_MAX, x_l, o,
+                                        mp);
     ws = o.ws;
     dprev_l = x_l;
     if (TRACE && active && l == 0 && P.trace) {

@@ -241,6 +241,20 @@ int cmpc_qp_solve_batch(int device, int n, int nu, int nqp, const double* H,
                         const uint32_t* ws_in, int max_chg, double* x,
                         int32_t* status, int32_t* nchg, uint32_t* ws_out,
                         uint8_t* trace, int32_t* ntrace);
+/* The same for one Jacobi-iteration solve (the map form of DESIGN.md §4):
+ * g = f + G d with G nqp*n*nvo (row-major per QP, columns in the order of the
+ * other sub-controllers' plans d, nqp*nvo: controller-major within each move,
+ * include/nerve_center.h:283-285).  Replaces ApplyOtherInput + SolveQP of
+ * DistributedSolver::UpdateAndSolveQP (include/distributed_solver.h:69-80,
+ * 98-103; libs/mpc_qp_solver.cc:42-75); bit-identical to the solves inside
+ * cmpc_iterate / cmpc_get_input.  nvo = 0: cmpc_qp_solve_batch. */
+int cmpc_qp_solve_batch_map(int device, int n, int nu, int nvo, int nqp,
+                            const double* H, const double* f, const double* G,
+                            const double* d, const double* lb, const double* ub,
+                            const double* lbA, const double* ubA,
+                            const uint32_t* ws_in, int max_chg, double* x,
+                            int32_t* status, int32_t* nchg, uint32_t* ws_out,
+                            uint8_t* trace, int32_t* ntrace);
 
 /* Upstream producer (host, untimed): AugmentedLinearizedSystem::Update for the
  * reference plants — linearise the plant at (x, u_full), discretise

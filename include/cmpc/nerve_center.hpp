@@ -421,27 +421,42 @@ class DistributedSolver : public MpcQpSolver {
   }
   /// UpdateAndSolveQP(qp, du_out, u_old, Su_other, du_other) (:69-80):
   /// ApplyOtherInput on *qp (f += G du_other; the caller passes a copy of
-  /// the step's QP, as distributed_controller.h:214 does), then SolveQP.
-  /// du_other: the other controllers' plans, controller-major, then move,
-  /// then input (nerve_center.h:283-285), m * (nu_tot - nu) values.
+  /// the step's QP, as distributed_controller.h:214 does), then the solve of
+  /// that Jacobi iteration: the map form of the iterate kernels
+  /// (cmpc_qp_solve_batch_map on the step's f, G and du_other), so the plan is
+  /// bit-identical to DistributedController::GetInput's.  du_other: the other
+  /// controllers' plans, controller-major, then move, then input
+  /// (nerve_center.h:283-285), m * (nu_tot - nu) values.
   void UpdateAndSolveQP(QP* qp, std::vector<double>* du_out, const double* u_old, const double* du_other) {
-    ApplyOtherInput(qp, du_other);
-    *du_out = SolveQP(*qp, u_old);
+    const int nV = L_.nV, nVo = L_.nVo;
+    if (!nVo) {
+      *du_out = SolveQP(*qp, u_old);
+      return;
+    }
+    if (static_cast<int>(qp->G.size()) != nV * nVo) throw Error("UpdateAndSolveQP: QP without G");
+    const std::vector<double> f0 = qp->f;  // the step's f
+    const std::vector<double> d = OtherPlans(du_other);
+    ApplyOtherInput(qp, d);
+    std::vector<double> x(nV);
+    SolveMap(*qp, f0.data(), d.data(), u_old, ws_, x.data());
+    *du_out = x;
   }
 
  private:
-  // f_k[a] = f[a] + sum_c G[a][c] du[c], c ascending over G's columns (move,
-  // then other input), each product rounded before the add: the order and
-  // rounding of the iterate kernel (cmpc_kernels.hip, f_k = f + G du_other)
-  void ApplyOtherInput(QP* qp, const double* du_other) {
+  // du_other (controller-major) in G's column order (move, then other input)
+  std::vector<double> OtherPlans(const double* du_other) const {
     const int nV = L_.nV, nVo = L_.nVo, nu = spec_.nu;
-    if (!nVo) return;
-    if (static_cast<int>(qp->G.size()) != nV * nVo) throw Error("UpdateAndSolveQP: QP without G");
     const int sm1 = nVo / nV, m = spec_.m;
     std::vector<double> d(nVo);
     for (int rk = 0; rk < sm1; ++rk)
       for (int mv = 0; mv < m; ++mv)
         for (int c = 0; c < nu; ++c) d[mv * (sm1 * nu) + rk * nu + c] = du_other[rk * nV + mv * nu + c];
+    return d;
+  }
+  // f_k[a] = f[a] + sum_c G[a][c] d[c], c ascending, each product rounded
+  // before the add (the reference's ApplyOtherInput on the caller's copy)
+  void ApplyOtherInput(QP* qp, const std::vector<double>& d) {
+    const int nV = L_.nV, nVo = L_.nVo;
     for (int a = 0; a < nV; ++a) {
       double t = qp->f[a];
       for (int c = 0; c < nVo; ++c) {
@@ -450,6 +465,26 @@ class DistributedSolver : public MpcQpSolver {
       }
       qp->f[a] = t;
     }
+  }
+  void SolveMap(const QP& qp, const double* f0, const double* d, const double* u_old, uint32_t ws_in, double* x) {
+    const int nV = L_.nV, nu = spec_.nu;
+    std::vector<double> lb(nV), ub(nV), lbA(nV), ubA(nV);
+    for (int i = 0; i < nV; ++i) {
+      lb[i] = c_.lower_bound[i % nu] - u_old[i % nu];
+      ub[i] = c_.upper_bound[i % nu] - u_old[i % nu];
+      lbA[i] = c_.lower_rate_bound[i % nu];
+      ubA[i] = c_.upper_rate_bound[i % nu];
+    }
+    int32_t status = 0, nchg = 0, ntrace = 0;
+    uint32_t ws_out = 0;
+    uint8_t trace[16];
+    Check(cmpc_qp_solve_batch_map(device_, nV, nu, L_.nVo, 1, qp.H.data(), f0, qp.G.data(), d, lb.data(), ub.data(),
+                                  lbA.data(), ubA.data(), &ws_in, CMPC_NWSR_MAX, x, &status, &nchg, &ws_out, trace,
+                                  &ntrace),
+          "cmpc_qp_solve_batch_map");
+    ws_ = ws_out;
+    status_ = status;
+    nchg_ = nchg;
   }
 };
 

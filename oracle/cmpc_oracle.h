@@ -93,6 +93,14 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
                 const double* lb, const double* ub, const double* lbA,
                 const double* ubA, uint32_t ws_in, int max_chg, double* x,
                 or_qp_info* info);
+/* The same QP with g = f + G d (G: n x nvo row-major, d: nvo), solved in the
+ * map form of the Jacobi iterations (or_qp.c header, step A); nvo = 0 is
+ * or_qp_solve. */
+#define CMPC_MAX_NVO 64
+int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
+                    const double* G, const double* d, const double* lb,
+                    const double* ub, const double* lbA, const double* ubA,
+                    uint32_t ws_in, int max_chg, double* x, or_qp_info* info);
 
 /* ---- batched NerveCenter step (or_nerve.c) ---- */
 typedef struct or_cfg {

@@ -15,26 +15,39 @@
  * (libs/mpc_qp_solver.cc:66-69), warm start from the previous working set of
  * the same QP slot (hotstart).
  *
- * Algorithm specification, version 2 (the HIP kernels implement the same
+ * Algorithm specification, version 3 (the HIP kernels implement the same
  * steps in the same arithmetic order):
  *   0. H = L D L' with reciprocal pivots R = 1/D (any pivot <= 0 -> NOT_PD);
- *      Hinv column by column from that factor.  x_u = -Hinv g.
+ *      Hinv column by column from that factor.
  *      nall_j = the normal of constraint j without its side: e_j (j < n),
  *      e_i (rate row i = j - n < nu), e_i - e_{i-nu} (rate row i >= nu).
  *      h_j = Hinv nall_j (a column or a difference of two columns).
  *   A. Warm start: slots = the constraints of ws_in in ascending j.  The
  *      working-set matrix M (M[i][k] = s_i s_k nall_{j_k}' h_{j_i} for
  *      i >= k, s = +1 lower side, -1 upper side) is factored M = L D L',
- *      reciprocal pivots R; a pivot <= 0 -> cold start (W empty, one change).
- *      lam = M^-1 (beta_W - N' x_u); while some lam_w < -tol_d: drop the most
+ *      reciprocal pivots R; a pivot d_j <= tol_z M_jj (dependent normals)
+ *      -> cold start (W empty, one change).
+ *      The gradient is g = f + G d (version 3): f, and G (n x nvo) times the
+ *      other sub-controllers' plans d, the Jacobi iteration's ApplyOtherInput
+ *      (include/distributed_solver.h:98-103); nvo = 0 for a plain QP.  The
+ *      working set's multipliers and point are affine in d (the map of W):
+ *        x_u0 = -Hinv f, U = Hinv G,
+ *        lam0 = M^-1 (beta_W - N' x_u0),  Lam = M^-1 N' U (one solve per
+ *        column), x0 = x_u0 + sum_a lam0_a h_a,  X = -U + sum_a Lam_a h_a,
+ *      lam = lam0 + Lam d.  If no lam_w < -tol_d: x = x0 + X d.  Else
+ *      x_u = x_u0 - U d and, while some lam_w < -tol_d: drop the most
  *      negative (lowest slot on ties) by the factor removal below, count one
- *      change, re-solve.  x = x_u + sum_a lam_a s_a h_{j_a}.
+ *      change, lam = M^-1 (beta_W - N' x_u); then x = x_u + sum_a lam_a h_a.
+ *      (h_a = s_a h_{j_a}; sums in ascending index order.)  A Jacobi loop
+ *      whose working set does not change evaluates only lam0 + Lam d and
+ *      x0 + X d per iteration; with nvo = 0 the map form is the plain
+ *      x_u, lam = M^-1 (beta_W - N' x_u), x = x_u + sum_a lam_a h_a.
  *   B. Repeat: pick the most violated inactive constraint p (slack < -tol_p,
  *      most negative; ties -> lowest j, lower side first).  None -> optimal.
  *      Goldfarb–Idnani step loop: hp = s_p h_p, qv = N'hp, r = M^-1 qv (the
  *      solve's scaled forward vector zz kept), z = hp - sum_a r_a s_a h_a,
  *      zn = nu_p'z, den = nu_p'hp, t1 = min_{r_a > tol_r} lam_a / r_a.
- *      If zn <= tol_z den (dependent): no blocking -> INFEASIBLE, else a dual
+ *      If zn <= tol_z den or K = n (dependent): no blocking -> INFEASIBLE, else a dual
  *      step t1 and the blocker is removed.  Else t2 = -slack_p * (1/zn),
  *      t = min(t1, t2) (t2 wins ties): x += t z, lam -= t r, u_p += t; a full
  *      step APPENDS p as the last slot (L row = zz, pivot zn, R = 1/zn: the
@@ -61,7 +74,7 @@
  *                over max(1, |r_a|)
  *   dependence   nu_p'z vs TOL_Z nu_p'Hinv nu_p over nu_p'Hinv nu_p
  *   step kind    t2 vs t1 over max(|t1|, |t2|)
- *   factor       the warm start's LDL' pivots over the diagonal of M
+ *   factor       the warm start's LDL' pivots vs TOL_Z M_aa over M_aa
  * (tests against a tolerance skip a rounding-noise zero: see mg_tol).
  * A QP whose inputs differ from another's by FP64 reassociation only
  * (~1e-13 relative) takes the same decisions whenever its margin is well
@@ -108,19 +121,21 @@ static void mg_tol(qp_t* q, double a, double thr, double scale) {
 }
 
 /* LDL' of the leading n x n block of a symmetric M (lower triangle read),
- * reciprocal pivots R = 1/D:
+ * reciprocal pivots R = 1/D; a pivot fails unless d_j > rel M_jj (rel = 0:
+ * H's positive definiteness; TOL_Z: a working set whose normals are
+ * dependent, e.g. a bound and a rate row with the same normal):
  *   d_j = M_jj - sum_{k<j} (L_jk L_jk) D_k,       R_j = 1 / d_j
  *   L_ij = (M_ij - sum_{k<j} (L_ik L_jk) D_k) R_j  (i > j), k ascending.
  * Returns -(j+1) for the first pivot d_j <= 0 (the rest still computed). */
 static int ldl(int n, double M[QMAX][QMAX], double L[QMAX][QMAX], double D[QMAX],
-               double R[QMAX]) {
+               double R[QMAX], double rel) {
   int rc = 0;
   for (int j = 0; j < n; ++j) {
     double d = M[j][j];
     for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
     D[j] = d;
     R[j] = 1.0 / d;
-    if (!(d > 0) && !rc) rc = -(j + 1);
+    if (!(d > rel * M[j][j]) && !rc) rc = -(j + 1);
     L[j][j] = 1.0;
     for (int i = j + 1; i < n; ++i) {
       double s = M[i][j];
@@ -196,11 +211,11 @@ static int wset_factor(qp_t* q, wset_t* W) {
     hinv_nu(q, W->j[i], W->side[i], h);
     for (int k = 0; k <= i; ++k) M[i][k] = nu_dot(q, W->j[k], W->side[k], h);
   }
-  const int rc = ldl(W->K, M, W->L, W->D, W->R);
-  /* margin of the pivot test d > 0 (pivots relative to M's diagonal), up
-   * to and including a failing pivot */
+  const int rc = ldl(W->K, M, W->L, W->D, W->R, TOL_Z);
+  /* margin of the pivot test d > TOL_Z M_aa (pivots relative to M's
+   * diagonal), up to and including a failing pivot */
   const int np = rc ? -rc : W->K;
-  for (int a = 0; a < np; ++a) mg(q, W->D[a], 0.0, fabs(M[a][a]));
+  for (int a = 0; a < np; ++a) mg(q, W->D[a], TOL_Z * M[a][a], fabs(M[a][a]));
   return rc;
 }
 
@@ -262,10 +277,10 @@ static void trace_push(or_qp_info* info, int add, int j, int side) {
     info->trace[info->ntrace++] = (uint8_t)((add ? 0x80 : 0) | (side ? 0x40 : 0) | j);
 }
 
-int or_qp_solve(int n, int nu, const double* H, const double* g,
-                const double* lb, const double* ub, const double* lbA,
-                const double* ubA, uint32_t ws_in, int max_chg, double* x_out,
-                or_qp_info* info) {
+int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
+                    const double* G, const double* d, const double* lb,
+                    const double* ub, const double* lbA, const double* ubA,
+                    uint32_t ws_in, int max_chg, double* x_out, or_qp_info* info) {
   qp_t q;
   wset_t W;
   double x[QMAX], xu[QMAX];
@@ -282,7 +297,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     double Hm[QMAX][QMAX], L[QMAX][QMAX], D[QMAX], R[QMAX];
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) Hm[i][j] = H[i * n + j];
-    const int rc = ldl(n, Hm, L, D, R);
+    const int rc = ldl(n, Hm, L, D, R, 0.0);
     for (int a = 0; a < (rc ? -rc : n); ++a) mg(&q, D[a], 0.0, fabs(H[a * n + a]));
     if (rc) {
       status = CMPC_QP_NOT_PD;
@@ -297,10 +312,20 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     for (int c = 0; c < n; ++c)
       for (int i = 0; i < c; ++i) q.Hinv[c][i] = q.Hinv[i][c];
   }
+  double xu0[QMAX], U[QMAX][CMPC_MAX_NVO], g[QMAX];
   for (int i = 0; i < n; ++i) {
     double s = 0;
-    for (int j = 0; j < n; ++j) s = s + q.Hinv[i][j] * g[j];
-    xu[i] = -s;
+    for (int j = 0; j < n; ++j) s = s + q.Hinv[i][j] * f[j];
+    xu0[i] = -s;
+    for (int c = 0; c < nvo; ++c) {
+      double u = 0;
+      for (int j = 0; j < n; ++j) u = u + q.Hinv[i][j] * G[j * nvo + c];
+      U[i][c] = u;
+    }
+    /* the gradient f + G d: the margin scales only (checker) */
+    double gi = f[i];
+    for (int c = 0; c < nvo; ++c) gi = gi + G[i * nvo + c] * d[c];
+    g[i] = gi;
   }
   double hmax = 0;
   for (int i = 0; i < n; ++i)
@@ -309,7 +334,7 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
   {
     double sx = 0, sg = 0;
     for (int i = 0; i < n; ++i) {
-      const double v[5] = {lb[i], ub[i], lbA[i], ubA[i], xu[i]};
+      const double v[5] = {lb[i], ub[i], lbA[i], ubA[i], xu0[i]};
       for (int k = 0; k < 5; ++k)
         if (isfinite(v[k]) && fabs(v[k]) > sx) sx = fabs(v[k]);
       if (fabs(g[i]) > sg) sg = fabs(g[i]);
@@ -330,35 +355,87 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
     W.K = 0;
     ++chg;
   }
-  for (;;) {
-    double rhs[QMAX], zz[QMAX];
+  {
+    /* the map of W: lam0, Lam (solves with the warm start's factor), then
+     * lam = lam0 + Lam d */
+    double rhs[QMAX], zz[QMAX], lam0[QMAX], Lam[QMAX][CMPC_MAX_NVO];
     for (int a = 0; a < W.K; ++a)
-      rhs[a] = beta(&q, W.j[a], W.side[a]) - nu_dot(&q, W.j[a], W.side[a], xu);
-    ldl_solve(W.K, W.L, W.R, rhs, W.lam, zz);
-    int worst = -1;
-    double wv = -tol_d;
-    for (int a = 0; a < W.K; ++a)
-      if (W.lam[a] < wv) {
-        wv = W.lam[a];
-        worst = a;
-      }
+      rhs[a] = beta(&q, W.j[a], W.side[a]) - nu_dot(&q, W.j[a], W.side[a], xu0);
+    ldl_solve(W.K, W.L, W.R, rhs, lam0, zz);
+    for (int c = 0; c < nvo; ++c) {
+      double uc[QMAX], lc[QMAX];
+      for (int r = 0; r < n; ++r) uc[r] = U[r][c];
+      for (int a = 0; a < W.K; ++a) rhs[a] = nu_dot(&q, W.j[a], W.side[a], uc);
+      ldl_solve(W.K, W.L, W.R, rhs, lc, zz);
+      for (int a = 0; a < W.K; ++a) Lam[a][c] = lc[a];
+    }
     for (int a = 0; a < W.K; ++a) {
-      mg_tol(&q, W.lam[a], -tol_d, q.s_lam);
-      if (worst >= 0 && a != worst && W.lam[a] < -tol_d) mg(&q, W.lam[a], wv, q.s_lam);
+      double v = lam0[a];
+      for (int c = 0; c < nvo; ++c) v = v + Lam[a][c] * d[c];
+      W.lam[a] = v;
     }
-    if (worst < 0) break;
-    trace_push(info, 0, W.j[worst], W.side[worst]);
-    wset_remove(&W, worst);
-    if (++chg > max_chg) {
-      status = CMPC_QP_MAX_NWSR;
-      goto done;
+    int first = 1, dropped = 0;
+    for (;;) {
+      if (!first) {
+        for (int a = 0; a < W.K; ++a)
+          rhs[a] = beta(&q, W.j[a], W.side[a]) - nu_dot(&q, W.j[a], W.side[a], xu);
+        ldl_solve(W.K, W.L, W.R, rhs, W.lam, zz);
+      }
+      first = 0;
+      int worst = -1;
+      double wv = -tol_d;
+      for (int a = 0; a < W.K; ++a)
+        if (W.lam[a] < wv) {
+          wv = W.lam[a];
+          worst = a;
+        }
+      for (int a = 0; a < W.K; ++a) {
+        mg_tol(&q, W.lam[a], -tol_d, q.s_lam);
+        if (worst >= 0 && a != worst && W.lam[a] < -tol_d) mg(&q, W.lam[a], wv, q.s_lam);
+      }
+      if (worst < 0) break;
+      if (!dropped) { /* leaving the map: x_u = x_u0 - U d */
+        for (int r = 0; r < n; ++r) {
+          double v = xu0[r];
+          for (int c = 0; c < nvo; ++c) v = v - U[r][c] * d[c];
+          xu[r] = v;
+        }
+        dropped = 1;
+      }
+      trace_push(info, 0, W.j[worst], W.side[worst]);
+      wset_remove(&W, worst);
+      if (++chg > max_chg) {
+        status = CMPC_QP_MAX_NWSR;
+        goto done;
+      }
     }
-  }
-  for (int r = 0; r < n; ++r) x[r] = xu[r];
-  for (int a = 0; a < W.K; ++a) {
-    double h[QMAX];
-    hinv_nu(&q, W.j[a], W.side[a], h);
-    for (int r = 0; r < n; ++r) x[r] = x[r] + W.lam[a] * h[r];
+    if (!dropped) { /* x = x0 + X d */
+      double x0[QMAX], X[QMAX][CMPC_MAX_NVO];
+      for (int r = 0; r < n; ++r) {
+        x0[r] = xu0[r];
+        for (int c = 0; c < nvo; ++c) X[r][c] = -U[r][c];
+      }
+      for (int a = 0; a < W.K; ++a) {
+        double h[QMAX];
+        hinv_nu(&q, W.j[a], W.side[a], h);
+        for (int r = 0; r < n; ++r) {
+          x0[r] = x0[r] + lam0[a] * h[r];
+          for (int c = 0; c < nvo; ++c) X[r][c] = X[r][c] + Lam[a][c] * h[r];
+        }
+      }
+      for (int r = 0; r < n; ++r) {
+        double v = x0[r];
+        for (int c = 0; c < nvo; ++c) v = v + X[r][c] * d[c];
+        x[r] = v;
+      }
+    } else {
+      for (int r = 0; r < n; ++r) x[r] = xu[r];
+      for (int a = 0; a < W.K; ++a) {
+        double h[QMAX];
+        hinv_nu(&q, W.j[a], W.side[a], h);
+        for (int r = 0; r < n; ++r) x[r] = x[r] + W.lam[a] * h[r];
+      }
+    }
   }
 
   /* B. Goldfarb–Idnani */
@@ -420,7 +497,9 @@ int or_qp_solve(int n, int nu, const double* H, const double* g,
           mg(&q, W.lam[a] * rv[k], W.lam[k] * rv[a], q.s_lam * fmax(rv[a], rv[k]));
       }
       mg_tol(&q, zn, TOL_Z * den, fabs(den));
-      if (zn <= TOL_Z * den) { /* nu_p dependent on the active normals */
+      /* nu_p dependent on the active normals (with n active constraints it
+       * is, whatever the rounding of zn) */
+      if (zn <= TOL_Z * den || W.K >= n) {
         if (k < 0) {
           status = CMPC_QP_INFEASIBLE;
           goto done;
@@ -485,4 +564,11 @@ done:
       if (W.j[a] < n) x[W.j[a]] = W.side[a] ? ub[W.j[a]] : lb[W.j[a]];
   for (int i = 0; i < n; ++i) x_out[i] = (status == CMPC_QP_OK) ? x[i] : 0.0;
   return status;
+}
+
+int or_qp_solve(int n, int nu, const double* H, const double* g,
+                const double* lb, const double* ub, const double* lbA,
+                const double* ubA, uint32_t ws_in, int max_chg, double* x_out,
+                or_qp_info* info) {
+  return or_qp_solve_map(n, nu, H, g, 0, NULL, NULL, lb, ub, lbA, ubA, ws_in, max_chg, x_out, info);
 }

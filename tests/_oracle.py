@@ -55,6 +55,9 @@ def lib():
                                   P(d), P(d), P(d)]
         L.or_qp_solve.argtypes = [ctypes.c_int, ctypes.c_int, P(d), P(d), P(d), P(d), P(d),
                                   P(d), u32, ctypes.c_int, P(d), P(OrQpInfo)]
+        L.or_qp_solve_map.argtypes = [ctypes.c_int, ctypes.c_int, P(d), P(d), ctypes.c_int, P(d),
+                                      P(d), P(d), P(d), P(d), P(d), u32, ctypes.c_int, P(d),
+                                      P(OrQpInfo)]
         L.or_step.argtypes = [P(CmpcDims), P(OrCfg), P(d), ctypes.c_int, u32, ctypes.c_int,
                               ctypes.c_int, P(d), P(d), P(u32), P(d), P(i32), P(i32),
                               P(ctypes.c_uint8), P(i32), P(d)]
@@ -125,6 +128,21 @@ def qp_solve(H, g, lb, ub, lbA, ubA, nu, ws_in=0, max_chg=10):
     c = lambda a: np.ascontiguousarray(a, dtype=np.float64)
     lib().or_qp_solve(n, nu, dptr(c(H)), dptr(c(g)), dptr(c(lb)), dptr(c(ub)), dptr(c(lbA)),
                       dptr(c(ubA)), int(ws_in), max_chg, dptr(x), ctypes.byref(info))
+    return x, info
+
+
+def qp_solve_map(H, f, G, d, lb, ub, lbA, ubA, nu, ws_in=0, max_chg=10):
+    """The Jacobi iteration's solve in the map form (or_qp.c step A): g = f + G d."""
+    n = len(f)
+    nvo = int(np.asarray(d).size)
+    x = np.zeros(n)
+    info = OrQpInfo()
+    c = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    Gc = c(np.asarray(G).reshape(n, nvo)) if nvo else None
+    dc = c(d) if nvo else None
+    lib().or_qp_solve_map(n, nu, dptr(c(H)), dptr(c(f)), nvo, dptr(Gc) if nvo else None,
+                          dptr(dc) if nvo else None, dptr(c(lb)), dptr(c(ub)), dptr(c(lbA)),
+                          dptr(c(ubA)), int(ws_in), max_chg, dptr(x), ctypes.byref(info))
     return x, info
 
 

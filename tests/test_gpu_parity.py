@@ -219,6 +219,48 @@ def test_gpu_solver_bitexact_on_identical_inputs():
             assert np.array_equal(x[q], xo), (q, x[q], xo)
 
 
+def test_gpu_map_form_solver_bitexact_on_identical_inputs():
+    """The Jacobi iteration's solve (map form, g = f + G d;
+    cmpc_qp_solve_batch_map, the solve of DistributedSolver::UpdateAndSolveQP)
+    == the oracle's or_qp_solve_map bit for bit, on the oracle's QPs with
+    plans d of several sizes and assorted warm starts (phase-A drops from the
+    map's multipliers, phase-B adds)."""
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 64
+    lin, u_old, _, _ = synthetic_batch(cfg, B, seed=6)
+    Ho, fo, Go = oracle_qps(cfg, arr, lin, u_old)
+    rng = np.random.default_rng(4)
+    n, nu = cfg.nV, cfg.nu
+    nq = B * cfg.S
+    lb = np.zeros((nq, n)); ub = np.zeros((nq, n)); lbA = np.zeros((nq, n)); ubA = np.zeros((nq, n))
+    for q in range(nq):
+        s = q % cfg.S
+        for mv in range(cfg.m):
+            lb[q, mv * nu:(mv + 1) * nu] = arr.lower[s] - u_old[q, :nu]
+            ub[q, mv * nu:(mv + 1) * nu] = arr.upper[s] - u_old[q, :nu]
+            lbA[q, mv * nu:(mv + 1) * nu] = arr.rate_lower[s]
+            ubA[q, mv * nu:(mv + 1) * nu] = arr.rate_upper[s]
+    total = 0
+    for scale in (0.01, 0.2, 2.0):
+        d = rng.normal(0, scale, (nq, cfg.nVo))
+        ws_in = np.zeros(nq, np.uint32)
+        for q in range(nq):
+            for j in rng.choice(2 * n, size=rng.integers(0, 3), replace=False):
+                ws_in[q] |= np.uint32(1 << int(j))
+                if rng.random() < 0.5:
+                    ws_in[q] |= np.uint32(1 << (16 + int(j)))
+        x, st, nchg, wso, tr, ntr = cmpc.qp_solve_batch_map(Ho, fo, Go, d, lb, ub, lbA, ubA, nu, ws_in)
+        for q in range(nq):
+            xo, info = O.qp_solve_map(Ho[q], fo[q], Go[q], d[q], lb[q], ub[q], lbA[q], ubA[q], nu, int(ws_in[q]))
+            assert st[q] == info.status and nchg[q] == info.nchg and wso[q] == info.ws, q
+            assert bytes(tr[q][:ntr[q]]) == bytes(info.trace[:info.ntrace]), q
+            assert np.array_equal(x[q], xo), (q, x[q], xo)
+        total += int(ntr.sum())
+    assert total > 50
+
+
 def test_gpu_solver_status_paths():
     """Zero move on every non-success (libs/mpc_qp_solver.cc:66-69)."""
     n, nu = 4, 2

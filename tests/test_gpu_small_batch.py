@@ -176,3 +176,92 @@ def test_gpu_fused_step_equals_split_step(plant, ctype, p, K, B):
             assert np.array_equal(x, y), (step, name)
     print(f"{plant}-{ctype} p={p} B={B}: ok {np.mean(split[-1][1] == 0):.3f}, "
           f"changes/QP {split[-1][7].sum() / len(split[-1][1]):.3f}")
+
+
+def _oracle_jacobi(cfg, arr, H, f, G, u_old, du_old, ws, K):
+    """The Jacobi loop of one step on the device's own (H, f, G) with the
+    oracle's map-form solve (or_qp.c step A, version 3): per iteration each
+    sub-controller solves with d = the other sub-controllers' previous plans
+    in G's column order (controller-major inside each move,
+    include/nerve_center.h:283-285)."""
+    import _oracle as O
+    S, nu, m = cfg.S, cfg.nu, cfg.m
+    nV = nu * m
+    nqp = H.shape[0]
+    dprev = du_old.reshape(nqp, nV).copy()
+    ws = ws.copy()
+    st = np.zeros(nqp, np.int32); nw = np.zeros(nqp, np.int32)
+    tr = np.full((nqp, K, 16), 0xFF, np.uint8); ntr = np.zeros((nqp, K), np.int32)
+    for k in range(K):
+        dnew = np.zeros_like(dprev)
+        for q in range(nqp):
+            b, s = divmod(q, S)
+            d = np.zeros((S - 1) * nV)
+            for rk in range(S - 1):
+                s2 = rk + (rk >= s)
+                for mv in range(m):
+                    d[mv * (S - 1) * nu + rk * nu: mv * (S - 1) * nu + rk * nu + nu] = \
+                        dprev[b * S + s2, mv * nu:(mv + 1) * nu]
+            lo = np.tile(arr.lower[s] - u_old[q, :nu], m); hi = np.tile(arr.upper[s] - u_old[q, :nu], m)
+            rlo = np.tile(arr.rate_lower[s], m); rhi = np.tile(arr.rate_upper[s], m)
+            x, info = O.qp_solve_map(H[q], f[q], G[q], d, lo, hi, rlo, rhi, nu, int(ws[q]))
+            dnew[q] = x
+            ws[q] = info.ws
+            st[q] = info.status; nw[q] = info.nchg
+            tr[q, k] = np.frombuffer(bytes(info.trace), np.uint8); ntr[q, k] = info.ntrace
+        dprev = dnew
+    return dprev, st, nw, ws, tr, ntr
+
+
+JCASES = [  # plant, controller, p, m, K, B scenarios
+    ("par", "coop", 20, 2, 9, 96),
+    ("par", "ncoop", 50, 2, 9, 48),
+    ("ser", "coop", 50, 2, 9, 48),
+    ("par", "coop", 30, 3, 9, 48),
+    ("par", "cent", 50, 2, 3, 64),
+    ("ser", "cent", 100, 2, 3, 48),
+]
+
+
+@pytest.mark.parametrize("plant,ctype,p,m,K,B", JCASES)
+@pytest.mark.parametrize("tight", [1.0, 0.3])
+@pytest.mark.parametrize("variant", ["lane", "rows"])
+def test_gpu_jacobi_map_form_bitexact_vs_oracle(plant, ctype, p, m, K, B, tight, variant):
+    """The iterate kernels' Jacobi solves against the oracle's map form on
+    the device's own QPs (identical inputs): every iteration's change
+    sequence, and the step's plans, statuses, change counts and working
+    sets, bit for bit, over three closed-loop steps with the first move
+    applied (the map of a working set kept and rebuilt across iterations on
+    the device, rebuilt per solve by the oracle)."""
+    cfg = cmpc.reference_config(plant, ctype, p=p, m=m)
+    arr = _tight(cmpc.controller_arrays(cfg, reference_setup(plant, ctype)), tight)
+    lin, u, du, ws = synthetic_batch(cfg, B, seed=70 + p + m, n_distinct=min(B, 512))
+    sv = cmpc.CMPC_SOLVE_LANE if variant == "lane" else cmpc.CMPC_SOLVE_ROWS
+    changes = 0
+    with cmpc.Context(cfg, B) as ctx:
+        ctx.configure(arr)
+        ctx.set_state(u, du, ws)
+        ctx.upload_lin(lin)
+        ctx.set_solve_variant(sv)
+        for step in range(3):
+            ctx.build()
+            if step == 0:
+                ctx.init_warmstart()
+            H, f, G = ctx.download_qp()
+            u0, du0, ws0 = (a.copy() for a in ctx.get_state())
+            ctx.iterate(K, cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE)
+            assert ctx.last_solve_kernel() == sv
+            d, st, nw = ctx.download()
+            tr, ntr = ctx.download_trace(K)
+            _, _, ws1 = ctx.get_state()
+            od, ost, onw, ows, otr, ontr = _oracle_jacobi(cfg, arr, H, f, G, u0, du0, ws0, K)
+            assert np.array_equal(ntr, ontr), (step, np.flatnonzero((ntr != ontr).any(1))[:8])
+            for q in range(len(st)):
+                for k in range(K):
+                    n = ntr[q, k]
+                    assert np.array_equal(tr[q, k, :n], otr[q, k, :n]), (step, q, k)
+            assert np.array_equal(st, ost) and np.array_equal(nw, onw), step
+            assert np.array_equal(ws1.view(np.uint32), ows.astype(np.uint32)), step
+            assert np.array_equal(d.reshape(od.shape), od), (step, np.abs(d.reshape(od.shape) - od).max())
+            changes += int(ntr.sum())
+    print(f"{plant}-{ctype} p={p} m={m} tight={tight} {variant}: {changes} working-set changes")

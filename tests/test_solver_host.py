@@ -76,3 +76,71 @@ def test_host_solver_bitexact_vs_oracle(n, nu):
         stats["active"] = stats.get("active", 0) + (ws != 0)
     # the sample exercises the constrained paths
     assert stats["active"] > 1000 and stats.get(0, 0) > 1000
+
+
+def host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg=10):
+    n, K = len(f), D.shape[0]
+    nvo = D.shape[1]
+    x = np.zeros((K, n))
+    st = np.zeros(K, np.int32); nchg = np.zeros(K, np.int32); ws = np.zeros(K, np.uint32)
+    ntr = np.zeros(K, np.int32); tr = np.zeros((K, 16), np.uint8)
+    P = ctypes.POINTER
+    rc = lib.qp_host_jacobi(n, nu, nvo, d(H), d(f), d(G if nvo else np.zeros(1)), d(D if nvo else np.zeros(1)), K,
+                            d(lb), d(ub), d(lbA), d(ubA), ctypes.c_uint32(ws_in), max_chg,
+                            x.ctypes.data_as(P(ctypes.c_double)), st.ctypes.data_as(P(ctypes.c_int32)),
+                            nchg.ctypes.data_as(P(ctypes.c_int32)), ws.ctypes.data_as(P(ctypes.c_uint32)),
+                            tr.ctypes.data_as(P(ctypes.c_uint8)), ntr.ctypes.data_as(P(ctypes.c_int32)))
+    assert rc == 0
+    return x, st, nchg, ws, tr, ntr
+
+
+@pytest.mark.parametrize("n,nu,nvo", [(4, 2, 4), (6, 2, 6), (8, 4, 0)])
+def test_host_jacobi_map_form_bitexact_vs_oracle(n, nu, nvo):
+    """The map form of the Jacobi iterations (qp_solve_map: the map of a
+    working set kept across the iterations, rebuilt on a change, the factor
+    restored after a solve that left it) against the oracle's stateless
+    or_qp_solve_map, iteration by iteration: bit-exact x, status, changes,
+    working set and change sequence.  The plans d mostly stay close (the map
+    is reused) and sometimes jump (working sets change, drops and adds in
+    phase A and B, returns to an earlier working set)."""
+    lib = host()
+    rng = np.random.default_rng(77 + n)
+    stats = {"hit": 0, "chg": 0}
+    for trial in range(400):
+        H, f, lb, ub, lbA, ubA = random_qp(rng, n, nu)
+        K = 9
+        G = rng.normal(0, 2.0, (n, max(nvo, 1)))[:, :nvo]
+        base = rng.normal(0, 0.3, nvo)
+        D = np.zeros((K, nvo))
+        for k in range(K):
+            jump = rng.random() < 0.3
+            D[k] = (rng.normal(0, 0.5, nvo) if jump else base + rng.normal(0, 1e-3, nvo)) if nvo else D[k]
+        ws_in = 0
+        if trial % 2:
+            for j in rng.choice(2 * n, size=rng.integers(0, n + 1), replace=False):
+                ws_in |= (1 << int(j)) | ((int(rng.integers(0, 2)) << (16 + int(j))))
+        max_chg = 10 if trial % 5 else int(rng.integers(0, 4))
+        xh, st, nchg, ws, tr, ntr = host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg)
+        w = ws_in
+        for k in range(K):
+            xo, info = O.qp_solve_map(H, f, G, D[k], lb, ub, lbA, ubA, nu, w, max_chg=max_chg)
+            assert st[k] == info.status, (trial, k)
+            assert nchg[k] == info.nchg, (trial, k)
+            assert ws[k] == info.ws, (trial, k)
+            assert bytes(tr[k, :ntr[k]]) == bytes(info.trace[:info.ntrace]), (trial, k)
+            assert np.array_equal(xh[k], xo), (trial, k, xh[k], xo)
+            stats["hit"] += int(k > 0 and info.nchg == 0 and w == info.ws)
+            stats["chg"] += int(info.nchg > 0)
+            w = info.ws
+    assert stats["hit"] > 1000 and stats["chg"] > 200, stats
+
+
+def test_map_form_without_other_plans_is_the_plain_solve():
+    """nvo = 0: the map form is the plain solve bit for bit (or_qp.c)."""
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        H, g, lb, ub, lbA, ubA = random_qp(rng, 8, 4)
+        ws_in = int(rng.integers(0, 1 << 16)) & 0xFFFF if trial % 2 else 0
+        x1, i1 = O.qp_solve(H, g, lb, ub, lbA, ubA, 4, ws_in)
+        x2, i2 = O.qp_solve_map(H, g, np.zeros((8, 0)), np.zeros(0), lb, ub, lbA, ubA, 4, ws_in)
+        assert np.array_equal(x1, x2) and i1.status == i2.status and i1.ws == i2.ws and i1.nchg == i2.nchg
