@@ -377,6 +377,48 @@ def cpp_step_latency(plant, ctype, p, steps=400):
     return out
 
 
+def recorded_run_changes(local, n_steps=10000):
+    """The solver load of the reference's own recorded run: the device closed
+    loop that reproduces results/parallel/run1/coop9.dat record for record
+    (cooperative parallel, p = 100, K = 9, the setup file's input step at
+    50 s, observer gain [0; I]; tests/test_closed_loop_golden.py), one
+    scenario, with the Jacobi iterations' working-set changes counted
+    (CMPC_TRACE) at every one of its n_steps instants."""
+    import cmpc
+    from cmpc.configs import reference_setup
+    from cmpc.driver import ClosedLoop
+    cfg = cmpc.reference_config("par", "coop")
+    setup = reference_setup("par", "coop")
+    arr = cmpc.controller_arrays(cfg, setup)
+    x0, u_def = cmpc.plant_default(cfg.plant)
+    M = cmpc.reference_observer_gain(cfg)
+    K = setup.n_iterations
+    loop = ClosedLoop(cfg, arr, [M] * cfg.S, x0[None, :], u_def[None, :], K, device=local)
+    per_step = []
+    t0 = time.perf_counter()
+    try:
+        loop.set_segments(setup.segments, u_def)
+        loop.initialize()
+        for _ in range(n_steps):
+            loop.step(trace=True)
+            per_step.append(loop.last_changes)
+        n_fail, _ = loop.plant_failures()
+    finally:
+        loop.close()
+    a = np.asarray(per_step)
+    return {"run": "results/parallel/run1/coop9.dat (cooperative parallel, p = 100, K = 9)",
+            "instants": int(n_steps), "S": cfg.S, "K": K,
+            "working_set_changes_total": int(a.sum()),
+            "working_set_changes_per_qp_step": float(a.sum()) / (n_steps * cfg.S),
+            "working_set_changes_per_qp_solve": float(a.sum()) / (n_steps * cfg.S * K),
+            "instants_with_a_change": int((a > 0).sum()),
+            "changes_first_100_instants": int(a[:100].sum()),
+            "plant_failures": n_fail, "seconds": time.perf_counter() - t0,
+            "note": "per_qp_step: changes summed over the K Jacobi iterations of one sub-controller's "
+                    "control step, averaged over the run's instants and sub-controllers (the synthetic "
+                    "headline's working_set_changes_per_qp_step is the same quantity)"}
+
+
 def run_configs(local, settle_seconds, steps, with_cpp=True):
     """SURVEY §8(d) / BASELINE.json configs 2, 3 and 5 at their batch sizes on
     this GPU, and (with_cpp) config 1 and the coop-par B = 1 step through the
@@ -589,9 +631,12 @@ def main():
     # working-set changes of the timed workload, summed over the K Jacobi
     # iterations and all QPs of a step (CMPC_TRACE counts, untimed pass over
     # one rotation of the batches)
-    ws_changes = None
+    ws_changes = ws_changes_steps = None
     if not args.headline_only:  # (profiler runs: every build launch a headline one, no traced solves)
-        ws_changes, _ = traced_changes(ctx, K, bind, range(first, first + NB))
+        # a traced replay of the timed steps from the same states: the moves
+        # applied over the timed steps shift u_old, so the later steps change
+        # working sets that the first rotation does not
+        ws_changes, ws_changes_steps = traced_changes(ctx, K, bind, range(first, first + args.steps))
         restore()
 
     # harder_qp: every state set meets other records at each of its steps
@@ -845,6 +890,12 @@ def main():
     configs = None
     if not args.no_configs and not args.headline_only and world == 1:
         configs = run_configs(local, args.settle_seconds, args.steps)
+    recorded = None
+    if not args.headline_only and world == 1:
+        try:
+            recorded = recorded_run_changes(local)
+        except Exception as e:  # reported, never required
+            log(f"recorded-run replay failed: {e}")
     coupled, rc, el_c = None, None, float("inf")
     if not args.no_coupled and not args.headline_only:
         from cmpc.coupled import run_coupled_bench
@@ -964,8 +1015,13 @@ def main():
         "u_old_max_drift_over_timed_steps": u_drift,
         "mean_working_set_changes_last_solve": mean_chg,
         "working_set_changes_per_step": ws_changes,
-        "working_set_changes_note": ("summed over all K Jacobi iterations and all QPs of one timed step "
-                                     "(CMPC_TRACE counts; untimed pass over one batch rotation)"),
+        "working_set_changes_per_qp_step": None if ws_changes is None else ws_changes / (B * S),
+        "working_set_changes_first_last_steps": (None if not ws_changes_steps else
+                                                 [ws_changes_steps[:NB], ws_changes_steps[-NB:]]),
+        "working_set_changes_note": ("summed over all K Jacobi iterations and all QPs of a timed step, "
+                                     "mean over a traced replay of all the timed steps from the same "
+                                     "states (CMPC_TRACE counts); per_qp_step = per step / (B S)"),
+        "recorded_run": recorded,
         "harder_qp": harder,
         "configs": configs,
         "closed_loop_device_resident": closed,

@@ -32,7 +32,7 @@ import time
 
 import numpy as np
 
-from . import Context
+from . import CMPC_TRACE, Context
 from .configs import ControllerConfig
 from .sim import REF_CONTROL_INDEX, REF_DELAYS, REF_EPS, REF_TS, PlantSimulator
 
@@ -133,9 +133,11 @@ class ClosedLoop:
         self.k = 0
         self.t_seg, self.seg_step = 0.0, 0   # integrate_const's start time and step count
 
-    def step(self):
+    def step(self, trace: bool = False):
         """One sampling instant: returns (t, y) of the instant; the plant has
-        advanced to the next one."""
+        advanced to the next one.  trace: the Jacobi iterations record their
+        working-set changes (CMPC_TRACE); self.last_changes is then their
+        total over the K iterations and all QP slots of this instant."""
         from ._abi import check, iptr
         t = 0.0 + self.k * self.Ts   # the record's label (record count)
         # integrate_const's own time: start_time + step * dt of the current
@@ -148,7 +150,10 @@ class ClosedLoop:
         self.sim.plant_input_offset(self.u_ctrl, self.u_offset, self.u_lin)
         self.ctx.observe_step(self.u_lin.data_ptr(), y.data_ptr())
         self.ctx.build()
-        self.ctx.iterate(self.K)
+        self.ctx.iterate(self.K, CMPC_TRACE if trace else 0)
+        if trace:
+            _, ntr = self.ctx.download_trace(self.K)
+            self.last_changes = int(ntr.sum())
         self.ctx.observe_apply()
         check(self.ctx.lib.cmpc_accumulate_moves(self.ctx._h, iptr(self.io),
                                                  self.torch_ptr(self.u_ctrl)), "cmpc_accumulate_moves")

@@ -195,7 +195,7 @@ struct cmpc_ctx {
   int last_solve = 0;                   // kernel launched by the last solve
   int step_variant = CMPC_STEP_AUTO;    // cmpc_set_step_variant
   int cus = 0;                          // compute units of the device (0: not yet queried)
-  std::vector<const void*> bound_ok;    // device pointers cmpc_bind_* validated before
+  std::vector<std::pair<const void*, size_t>> bound_ok;  // (device pointer, bytes) cmpc_bind_* validated before
   bool lds_layout_ok = false;           // lds_layout holds build_lds_layout(d, L)
   BuildParams lds_layout{};             // (a function of the dimensions only)
   int last_step_fused = 0;
@@ -425,10 +425,6 @@ int cmpc_create(cmpc_ctx** out, const cmpc_dims* dims, int device) {
     cmpc_destroy(c);
     return rc;
   };
-  // (experiment: CMPC_SPIN_WAIT=1 asks the runtime to spin instead of block
-  // in its waits; it takes effect only before the device's first use)
-  if (const char* e = std::getenv("CMPC_SPIN_WAIT"))
-    if (e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   if (hipSetDevice(device) != hipSuccess) return cleanup(fail("hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail("hipStreamCreate failed"));
@@ -619,26 +615,35 @@ int cmpc_download_lin(cmpc_ctx* c, double* lin) {
 
 void* cmpc_lin_device(cmpc_ctx* c) { return c ? (void*)c->lin : nullptr; }
 
-// p is device memory of the context's device.  A rotation over a few bound
-// buffers (the bench binds four per step) queries each once: the runtime's
-// pointer lookup is several microseconds of host time per call, more than a
-// small batch's kernels take
-static bool device_ptr_ok(cmpc_ctx* c, const void* p) {
-  for (const void* v : c->bound_ok)
-    if (v == p) return true;
+// p is device memory of the context's device and [p, p + bytes) lies inside
+// its allocation.  A rotation over a few bound buffers (the bench binds four
+// per step) queries each (pointer, size) once: the runtime's lookups are
+// several microseconds of host time per call, more than a small batch's
+// kernels take.  A pointer is therefore validated the first time it is bound
+// to this context (include/cmpc.h, cmpc_bind_lin): a caller that frees a
+// bound buffer and binds another allocation at the same address must make
+// it at least as large.
+static bool device_ptr_ok(cmpc_ctx* c, const void* p, size_t bytes) {
+  for (const auto& v : c->bound_ok)
+    if (v.first == p && v.second >= bytes) return true;
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice || a.device != c->device)
     return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base &&
+      (uintptr_t)p + bytes > (uintptr_t)base + size)
+    return false;
   if (c->bound_ok.size() >= 64) c->bound_ok.erase(c->bound_ok.begin());
-  c->bound_ok.push_back(p);
+  c->bound_ok.emplace_back(p, bytes);
   return true;
 }
 
 int cmpc_bind_lin(cmpc_ctx* c, const double* lin_device) {
   if (!c) return fail("null context");
   if (lin_device) {
-    if (!device_ptr_ok(c, lin_device))
-      return fail("cmpc_bind_lin: not a device pointer on the context's device");
+    if (!device_ptr_ok(c, lin_device, sizeof(double) * (size_t)c->nqp * c->L.rec_len))
+      return fail("cmpc_bind_lin: not a device allocation of nqp * rec_len doubles on the context's device");
     // the build kernels read records with 16-byte loads (LDS-DMA / double2)
     if (reinterpret_cast<uintptr_t>(lin_device) % 16 != 0)
       return fail("cmpc_bind_lin: records must be 16-byte aligned");
@@ -657,9 +662,10 @@ int cmpc_bind_state(cmpc_ctx* c, double* u_old, double* du_old, uint32_t* ws) {
     return 0;
   }
   if (nnull != 0) return fail("cmpc_bind_state: bind all three state arrays or none");
-  const void* ptrs[] = {u_old, du_old, ws};
-  for (const void* p : ptrs)
-    if (!device_ptr_ok(c, p)) return fail("cmpc_bind_state: not a device pointer on the context's device");
+  const size_t n = (size_t)c->nqp;
+  if (!device_ptr_ok(c, u_old, sizeof(double) * n * c->d.nu_tot) ||
+      !device_ptr_ok(c, du_old, sizeof(double) * n * c->L.nV) || !device_ptr_ok(c, ws, sizeof(uint32_t) * n))
+    return fail("cmpc_bind_state: not device allocations of the state's size on the context's device");
   if (reinterpret_cast<uintptr_t>(u_old) % 8 || reinterpret_cast<uintptr_t>(du_old) % 8 ||
       reinterpret_cast<uintptr_t>(ws) % 4)
     return fail("cmpc_bind_state: misaligned state array");

@@ -51,20 +51,25 @@ inline int cmpc_blocks_per_cu(F kernel, int threads, size_t lds) {
   return v;
 }
 
-// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, size):
-// a launcher that set it on every launch paid its host time per step (a
-// config-5 step: 57 us of wall time per 41 us kernel)
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel,
+// size): a launcher that set it on every launch paid its host time per step
+// (a config-5 step: 57 us of wall time per 41 us kernel).  The attribute
+// belongs to the function object of the current device, so a host thread
+// that drives contexts on two devices sets it on each.
 inline void cmpc_allow_lds(const void* kernel, size_t bytes) {
   struct Entry {
+    int dev;
     const void* k;
     size_t bytes;
   };
   static thread_local Entry cache[32];
   static thread_local int n = 0;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
   for (int i = 0; i < n && i < 32; ++i)
-    if (cache[i].k == kernel && cache[i].bytes >= bytes) return;
+    if (cache[i].dev == dev && cache[i].k == kernel && cache[i].bytes >= bytes) return;
   (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  cache[n % 32] = Entry{kernel, bytes};
+  cache[n % 32] = Entry{dev, kernel, bytes};
   ++n;
 }
 

@@ -678,11 +678,17 @@ void cmpc_control_step_kernel(ControlStepParams C) {
                                   blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
   __syncthreads();
   build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(C.b);
+  // polled completion: each wave's result stores (du, status, nWSR in
+  // page-locked host memory; waves 1-3 store theirs when the block has 2-4
+  // centralized QPs) are released at system scope by the wave itself, before
+  // the barrier that orders them ahead of wave 0's done store (a workgroup
+  // barrier does not wait for other waves' outstanding global stores)
+  if (C.done) __threadfence_system();
   __syncthreads();
   if (wave == 0) {
     obs_prior_row<NS, NUT>(C.ob, blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
-    // every wave's results were stored before the barrier above, wave 0's
-    // a-priori stores before this release (a vector store, system scope)
+    // wave 0's a-priori stores before this release (a vector store, system
+    // scope)
     if (C.done && lane == 0) __hip_atomic_store(C.done, C.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }

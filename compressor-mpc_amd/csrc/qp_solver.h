@@ -39,6 +39,7 @@ CMPC_HD double sel(const double (&v)[N], int i) {
 // lane-contiguous LDS array (the solve kernel, to keep 2 waves/SIMD).
 template <int N>
 struct HinvRegs {
+  static constexpr bool kColumns = false;  // H^-1 nu by the explicit normal (register-indexed)
   double m[N][N];
   CMPC_HD double operator()(int r, int c) const { return m[r][c]; }
   CMPC_HD void set(int r, int c, double v) { m[r][c] = v; }
@@ -48,6 +49,7 @@ struct HinvRegs {
 // needs H^-1 only to build a map and off the common path
 template <int N, int STRIDE>
 struct HinvStrided {
+  static constexpr bool kColumns = true;  // H^-1 nu by column reads (runtime addresses)
   double* p;
   CMPC_HD double operator()(int r, int c) const { return r <= c ? p[(r * N + c) * STRIDE] : p[(c * N + r) * STRIDE]; }
   CMPC_HD void set(int r, int c, double v) {
@@ -61,6 +63,7 @@ struct HinvStrided {
 template <int N, int NU, int NB = N, class HS = HinvRegs<N>>
 struct Qp {
   static_assert(NB == N || NB == NU, "bounds: general or NU-periodic");
+  using HS_t = HS;
   HS Hinv;
   double lb[NB], ub[NB], lbA[NB], ubA[NB];
   // phase-B violation thresholds -TOL_P (1 + |beta|) per bound and side,
@@ -99,6 +102,19 @@ struct Qp {
 #pragma unroll
     for (int c = 0; c < N; ++c)
       n[c] = (c == i) ? sg : ((rate && i >= NU && c == i - NU) ? -sg : 0.0);
+  }
+  // out = Hinv nu_{j,side} by columns (or_qp.c hinv_nu: a column, or a
+  // difference of two columns, negated for the upper side); the same values
+  // as hinv_n on the explicit normal
+  CMPC_HD void hcol(int j, int side, double (&out)[N]) const {
+    const bool rate = j >= N;
+    const int i = rate ? j - N : j;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double t = Hinv(r, i);
+      if (rate && i >= NU) t = t - Hinv(r, i - NU);
+      out[r] = side ? -t : t;
+    }
   }
   // out = Hinv n
   CMPC_HD void hinv_n(const double (&n)[N], double (&out)[N]) const {
@@ -159,6 +175,38 @@ template <int N, bool SN, class Q>
 CMPC_HD double wset_beta(const Q& q, const WSet<N, SN>& W, int a) {
   if constexpr (SN) return W.bta[a];
   else return q.beta(W.j[a], W.side[a]);
+}
+
+// H^-1 n_a of slot a: columns of an LDS-resident H^-1 (runtime addresses),
+// else the explicit normal's product (registers take compile-time indices)
+template <int N, bool SN, class Q>
+CMPC_HD void wset_h(const Q& q, const WSet<N, SN>& W, int a, double (&out)[N]) {
+  if constexpr (Q::HS_t::kColumns) {
+    q.hcol(W.j[a], W.side[a], out);
+  } else {
+    double n[N];
+    wset_normal(q, W, a, n);
+    q.hinv_n(n, out);
+  }
+}
+// n_a' v of slot a (the explicit normal's FMAs: fewer instructions than
+// selecting v's entries by the runtime constraint index)
+template <int N, bool SN, class Q>
+CMPC_HD double wset_dot(const Q& q, const WSet<N, SN>& W, int a, const double (&v)[N]) {
+  double n[N];
+  wset_normal(q, W, a, n);
+  return ndot<N>(n, v);
+}
+// H^-1 nu_{j,side}
+template <int N, class Q>
+CMPC_HD void q_h(const Q& q, int j, int side, double (&out)[N]) {
+  if constexpr (Q::HS_t::kColumns) {
+    q.hcol(j, side, out);
+  } else {
+    double n[N];
+    q.normal(j, side, n);
+    q.hinv_n(n, out);
+  }
 }
 
 // LDL' of the leading K x K block of M (lower triangle read) with reciprocal
@@ -243,11 +291,7 @@ CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
 #pragma unroll
   for (int b = 0; b < N; ++b) {
     double hb[N];
-    if (b < W.K) {
-      double nb[N];
-      wset_normal(q, W, b, nb);
-      q.hinv_n(nb, hb);
-    }
+    if (b < W.K) wset_h(q, W, b, hb);
 #pragma unroll
     for (int a = 0; a <= b; ++a) {
       double v = 0.0;
@@ -451,9 +495,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
     for (int a = 0; a < N; ++a) {
       rhs[a] = 0.0;
       if (a < W.K) {
-        double na[N];
-        wset_normal(q, W, a, na);
-        rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu);
+        rhs[a] = wset_beta(q, W, a) - wset_dot(q, W, a, xu);
       }
     }
     ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
@@ -488,9 +530,8 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
 #pragma unroll
     for (int a = 0; a < N; ++a) {
       if (a < W.K) {
-        double na[N], ha[N];
-        wset_normal(q, W, a, na);
-        q.hinv_n(na, ha);
+        double ha[N];
+        wset_h(q, W, a, ha);
 #pragma unroll
         for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
       }
@@ -544,18 +585,12 @@ CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[
     double up = 0.0;
     for (int inner = 0; inner <= max_chg + 1 && !done; ++inner) {
       double hp[N], qv[N], rv[N], zz[N], z[N];
-      {
-        double np_[N];  // (rebuilt here: registers)
-        q.normal(pj, ps, np_);
-        q.hinv_n(np_, hp);
-      }
+      q_h<N>(q, pj, ps, hp);
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         qv[a] = 0.0;
         if (a < W.K) {
-          double na[N];
-          wset_normal(q, W, a, na);
-          qv[a] = ndot<N>(na, hp);
+          qv[a] = wset_dot(q, W, a, hp);
         }
       }
       ldl_solve_k<N>(W.K, W.L, W.R, qv, rv, zz);
@@ -564,9 +599,8 @@ CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         if (a < W.K) {
-          double na[N], ha[N];
-          wset_normal(q, W, a, na);
-          q.hinv_n(na, ha);
+          double ha[N];
+          wset_h(q, W, a, ha);
 #pragma unroll
           for (int r = 0; r < N; ++r) z[r] = z[r] - rv[a] * ha[r];
         }
@@ -712,36 +746,38 @@ struct UStrided {
   CMPC_HD double operator()(int r, int c) const { return p[(r * NVOA + c) * STRIDE]; }
 };
 
-// the map of the WSet's slots (fresh warm-start factor)
+// the map of the WSet's slots (fresh warm-start factor).  Each slot's
+// explicit normal is formed once and serves all 1 + NVO right-hand sides
+// (N' x_u0 and N' U's columns: FMAs with 0 / +-1 coefficients, exact, the
+// oracle's nu_dot values).
 template <int N, int NVO, int NU, int NB, class HS, bool SN, class UA>
 CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const double (&xu0)[N],
                         const UA& U, JMap<N, NVO>& mp) {
-  double rhs[N];
+  constexpr int NVOA = JMap<N, NVO>::NVOA;
+  double rhs0[N], rc[NVOA][N];
 #pragma unroll
   for (int a = 0; a < N; ++a) {
-    rhs[a] = 0.0;
+    rhs0[a] = 0.0;
+#pragma unroll
+    for (int c = 0; c < NVOA; ++c) rc[c][a] = 0.0;
     if (a < W.K) {
       double na[N];
       wset_normal(q, W, a, na);
-      rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu0);
-    }
-  }
-  ldl_solve_k<N>(W.K, W.L, W.R, rhs, mp.lam0);
+      rhs0[a] = wset_beta(q, W, a) - ndot<N>(na, xu0);
 #pragma unroll
-  for (int c = 0; c < NVO; ++c) {
-    double uc[N], lc[N];
+      for (int c = 0; c < NVO; ++c) {
+        double uc[N];
 #pragma unroll
-    for (int r = 0; r < N; ++r) uc[r] = U(r, c);
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-      rhs[a] = 0.0;
-      if (a < W.K) {
-        double na[N];
-        wset_normal(q, W, a, na);
-        rhs[a] = ndot<N>(na, uc);
+        for (int r = 0; r < N; ++r) uc[r] = U(r, c);
+        rc[c][a] = ndot<N>(na, uc);
       }
     }
-    ldl_solve_k<N>(W.K, W.L, W.R, rhs, lc);
+  }
+  ldl_solve_k<N>(W.K, W.L, W.R, rhs0, mp.lam0);
+#pragma unroll
+  for (int c = 0; c < NVO; ++c) {
+    double lc[N];
+    ldl_solve_k<N>(W.K, W.L, W.R, rc[c], lc);
 #pragma unroll
     for (int a = 0; a < N; ++a) mp.Lam[a][c] = lc[a];  // zero from K on
   }
@@ -754,9 +790,8 @@ CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const 
 #pragma unroll
   for (int a = 0; a < N; ++a) {
     if (a < W.K) {
-      double na[N], ha[N];
-      wset_normal(q, W, a, na);
-      q.hinv_n(na, ha);
+      double ha[N];
+      wset_h(q, W, a, ha);
 #pragma unroll
       for (int r = 0; r < N; ++r) {
         mp.x0[r] = mp.x0[r] + mp.lam0[a] * ha[r];
@@ -867,20 +902,10 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
       return;
     }
   }
-  // off the map: the map is dropped (its registers are free for the slow
-  // path; after a working-set change the next ws_in is another anyway), and
-  // the working set of ws_in is rebuilt with its fresh factor
+  // off the map: the map is dropped (after a working-set change the next
+  // ws_in is another anyway), and the working set of ws_in is rebuilt with
+  // its fresh factor
   mp.ws = kWsInvalid;
-#pragma unroll
-  for (int a = 0; a < N; ++a) {
-    mp.lam0[a] = 0.0;
-    mp.x0[a] = 0.0;
-#pragma unroll
-    for (int c = 0; c < JMap<N, NVO>::NVOA; ++c) {
-      mp.Lam[a][c] = 0.0;
-      mp.X[a][c] = 0.0;
-    }
-  }
   if (!have_w) {
     wset_fill(q, ws_in, W);
     wset_factor<N>(q, W);  // (succeeded when the map was built)
@@ -904,9 +929,7 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
         for (int a = 0; a < N; ++a) {
           rhs[a] = 0.0;
           if (a < W.K) {
-            double na[N];
-            wset_normal(q, W, a, na);
-            rhs[a] = wset_beta(q, W, a) - ndot<N>(na, xu);
+            rhs[a] = wset_beta(q, W, a) - wset_dot(q, W, a, xu);
           }
         }
         ldl_solve_k<N>(W.K, W.L, W.R, rhs, W.lam);
@@ -940,9 +963,8 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         if (a < W.K) {
-          double na[N], ha[N];
-          wset_normal(q, W, a, na);
-          q.hinv_n(na, ha);
+          double ha[N];
+          wset_h(q, W, a, ha);
 #pragma unroll
           for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
         }

@@ -153,7 +153,10 @@ int cmpc_download_lin(cmpc_ctx* ctx, double* lin_host);
 /* Bind an external device-resident record array (B*S*rec_len doubles on the
  * ctx device, 16-byte aligned, e.g. the output of a device-side producer);
  * NULL re-binds the context's own buffer.  Takes effect for the next
- * cmpc_build. */
+ * cmpc_build.  cmpc_bind_lin and cmpc_bind_state check that each pointer is
+ * device memory of the context's device inside an allocation of the
+ * required size, once per (pointer, size) and context: re-binding a buffer
+ * freed and re-allocated at the same address is not re-checked. */
 int cmpc_bind_lin(cmpc_ctx* ctx, const double* lin_device);
 
 /* Hot path. */

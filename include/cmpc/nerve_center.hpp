@@ -9,7 +9,8 @@
 //   NerveCenter ctor (controllers, n_solver_iterations) include/nerve_center.h:89-95
 //   DistributedController(sys, constraints, M)         include/distributed_controller.h:126-128
 //   DistributedController::{Initialize, SetWeights, SetOutputReference,
-//     UpdateU, GenerateInitialQP, GetInput, GetStateEstimate}
+//     UpdateU, GenerateInitialQP, GetInput, GetStateEstimate}, incl. the
+//     timed overloads on a CpuTimer (boost::timer::cpu_timer's role)
 //                                                       include/distributed_controller.h:131-191
 //   NerveCenter::Initialize(x, u, u_full, y, dx)      include/nerve_center.h:98-104
 //   NerveCenter::SetWeights(uwt, ywt)                 include/nerve_center.h:107-110
@@ -65,6 +66,51 @@ inline void Check(int rc, const char* what) {
     throw Error(std::string(what) + ": " + (m ? m : "error"));
   }
 }
+
+// The reference's boost::timer::cpu_timer as its harness uses it (the timed
+// overloads of DistributedController, distributed_controller.h:155-183, and
+// NerveCenter's per-controller helpers, nerve_center.h:261-310): a wall clock
+// that accumulates between resume() and stop().  Boost is not a dependency
+// here; elapsed().wall is in nanoseconds like boost's cpu_times::wall.
+class CpuTimer {
+ public:
+  struct Times {
+    int64_t wall = 0;  // nanoseconds
+  };
+  CpuTimer() { start(); }
+  /// (re)start from zero, running (boost: start()).
+  void start() {
+    acc_ = 0;
+    stopped_ = false;
+    t0_ = std::chrono::steady_clock::now();
+  }
+  /// stop accumulating (boost: stop()); no-op when stopped.
+  void stop() {
+    if (stopped_) return;
+    acc_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_).count();
+    stopped_ = true;
+  }
+  /// continue accumulating (boost: resume()); no-op when running.
+  void resume() {
+    if (!stopped_) return;
+    stopped_ = false;
+    t0_ = std::chrono::steady_clock::now();
+  }
+  bool is_stopped() const { return stopped_; }
+  /// the accumulated time, including the running interval (boost: elapsed()).
+  Times elapsed() const {
+    Times t;
+    t.wall = acc_;
+    if (!stopped_)
+      t.wall += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_).count();
+    return t;
+  }
+
+ private:
+  int64_t acc_ = 0;
+  bool stopped_ = false;
+  std::chrono::steady_clock::time_point t0_{};
+};
 
 enum class PlantType { Parallel = CMPC_PLANT_PARALLEL, Serial = CMPC_PLANT_SERIAL };
 enum class ControllerType { Centralized, Cooperative, NonCooperative };
@@ -574,12 +620,27 @@ class DistributedController {
   /// UpdateU(du) (:146-152): ObserveAPriori(du, u_old_), u_old_ += du; du is
   /// nu_tot in this controller's order.
   void UpdateU(const double* du) { Check(cmpc_update_u_host(dev().ctx, du), "cmpc_update_u_host"); }
+  /// UpdateU(time_out, du) (:155-159): the same, with time_out resumed
+  /// around it (the reference's boost::timer::cpu_timer -> CpuTimer).
+  void UpdateU(CpuTimer* time_out, const double* du) {
+    time_out->resume();
+    UpdateU(du);
+    time_out->stop();
+  }
   /// GenerateInitialQP(y, full_u_old) (distributed_controller.cc:72-108):
   /// a-posteriori observer update, linearisation at the estimate, the QP.
   void GenerateInitialQP(const double* y, const double* full_u_old) {
     Device& D = dev();
     Check(cmpc_observe_step_host(D.ctx, full_u_old, y), "cmpc_observe_step_host");
     Check(cmpc_build(D.ctx), "cmpc_build");
+  }
+  /// GenerateInitialQP(time_out, y, full_u_old) (:165-170): timed; the
+  /// build is complete on the device when the timer stops.
+  void GenerateInitialQP(CpuTimer* time_out, const double* y, const double* full_u_old) {
+    time_out->resume();
+    GenerateInitialQP(y, full_u_old);
+    Check(cmpc_synchronize(dev().ctx), "cmpc_synchronize");
+    time_out->stop();
   }
   /// GetInput(&u_solution, du_last) (:173-183, :206-226): the QP with the other
   /// controllers' plans du_last (m * (nu_tot - nu) values, controller-major;
@@ -589,6 +650,12 @@ class DistributedController {
     Device& D = dev();
     Check(cmpc_get_input_host(D.ctx, D.L.nVo > 0 ? du_last : nullptr, 0u), "cmpc_get_input_host");
     Check(cmpc_download(D.ctx, u_solution, &D.status, &D.nwsr), "cmpc_download");
+  }
+  /// GetInput(time_out, &u_solution, du_last) (:176-183): timed.
+  void GetInput(CpuTimer* time_out, double* u_solution, const double* du_last) {
+    time_out->resume();
+    GetInput(u_solution, du_last);
+    time_out->stop();
   }
   /// GetStateEstimate() (:186-191): the observer's x_ (ns values).
   std::vector<double> GetStateEstimate() {

@@ -7,6 +7,7 @@
 //   GenerateInitialQP(y, u_full_old) per controller,
 //   K x { GetInput(&du_s, du_prev without its own segment) },
 //   UpdateUOld, SendUHelper: UpdateU(du with only the own inputs set),
+//   on odd steps through the timed overloads (CpuTimer),
 // and checks, step by step, that the applied inputs, the move plans, the QP
 // status words and every controller's GetStateEstimate equal NerveCenter's
 // bit for bit.  Beside each controller runs a DistributedSolver (the
@@ -118,7 +119,17 @@ int main(int argc, char** argv) {
     // NerveCenter's own state for the hand-driven loop (nerve_center.h:71-75)
     std::vector<double> u_old(nut, 0.0), du_old(static_cast<size_t>(S) * nV, 0.0);
     bool all_equal = true;
+    // odd steps run (b) through the timed overloads (distributed_controller.h:
+    // 155-183) with one CpuTimer per controller and phase, as the reference's
+    // TimeInitializeQPHelper / TimeSolveQPHelper would (nerve_center.h:261-310)
+    std::vector<CpuTimer> t_build(S), t_solve(S), t_update(S);
+    for (int s = 0; s < S; ++s) {
+      t_build[s].stop();
+      t_solve[s].stop();
+      t_update[s].stop();
+    }
     for (int k = 0; k < steps; ++k) {
+      const bool timed = k % 2 == 1;
       std::vector<double> y(y0);
       for (int o = 0; o < spec.n_outputs; ++o) y[o] = y0[o] * (1.0 + 2e-3 * std::sin(1.3 * k + o));
       // (a)
@@ -128,7 +139,8 @@ int main(int argc, char** argv) {
       for (int c = 0; c < nut; ++c) u_full[spec.plant_input_index[c]] += u_old[c];
       std::vector<std::vector<double>> uo_s(S);
       for (int s = 0; s < S; ++s) {
-        ctrl[s].GenerateInitialQP(y.data(), u_full.data());
+        if (timed) ctrl[s].GenerateInitialQP(&t_build[s], y.data(), u_full.data());
+        else ctrl[s].GenerateInitialQP(y.data(), u_full.data());
         uo_s[s] = ctrl[s].GetUOld();
         ds[s].GenerateDistributedQP(&qps[s], ctrl[s].GetLinRecord().data(), uo_s[s].data());
         solver_equal = solver_equal && same_qp(qps[s], ctrl[s].GetQP());
@@ -140,7 +152,8 @@ int main(int argc, char** argv) {
           std::vector<double> du_last;  // the others' plans, controller-major (:283-285)
           for (int s2 = 0; s2 < S; ++s2)
             if (s2 != s) du_last.insert(du_last.end(), du_prev.begin() + s2 * nV, du_prev.begin() + (s2 + 1) * nV);
-          ctrl[s].GetInput(du_new.data() + s * nV, du_last.empty() ? nullptr : du_last.data());
+          if (timed) ctrl[s].GetInput(&t_solve[s], du_new.data() + s * nV, du_last.empty() ? nullptr : du_last.data());
+          else ctrl[s].GetInput(du_new.data() + s * nV, du_last.empty() ? nullptr : du_last.data());
           status[s] = ctrl[s].last_status();
           // the same solve through the reference's solver API, on a copy of
           // the step's QP (distributed_controller.h:214)
@@ -165,7 +178,8 @@ int main(int argc, char** argv) {
       for (int s = 0; s < S; ++s) {
         std::vector<double> du_s(nut, 0.0);
         for (int c = 0; c < nu; ++c) du_s[c] = du_applied[spec.input_order[s][c]];
-        ctrl[s].UpdateU(du_s.data());
+        if (timed) ctrl[s].UpdateU(&t_update[s], du_s.data());
+        else ctrl[s].UpdateU(du_s.data());
       }
       // compare
       bool eq = u_nc == u_old && nc.last_plans() == du_old;
@@ -179,11 +193,21 @@ int main(int argc, char** argv) {
       for (double v : u_old) std::printf(" %.9g", v);
       std::printf("  status");
       for (int v : status) std::printf(" %d", v);
-      std::printf("  %s (max |du| %.3g)  solver API %s\n", eq ? "equal" : "DIFFERENT", dmax,
-                  solver_equal ? "equal" : "DIFFERENT");
+      std::printf("  %s (max |du| %.3g)  solver API %s%s\n", eq ? "equal" : "DIFFERENT", dmax,
+                  solver_equal ? "equal" : "DIFFERENT", timed ? "  (timed overloads)" : "");
       all_equal = all_equal && eq && solver_equal;
     }
-    return all_equal ? 0 : 3;
+    for (int s = 0; s < S; ++s)
+      std::printf("controller %d timed overloads: GenerateInitialQP %.1f us, GetInput %.1f us, UpdateU %.1f us "
+                  "(summed over the timed steps)\n",
+                  s, t_build[s].elapsed().wall * 1e-3, t_solve[s].elapsed().wall * 1e-3,
+                  t_update[s].elapsed().wall * 1e-3);
+    bool timers_ok = true;
+    for (int s = 0; s < S; ++s)
+      timers_ok = timers_ok && (steps < 2 || (t_build[s].elapsed().wall > 0 && t_solve[s].elapsed().wall > 0 &&
+                                             t_update[s].elapsed().wall > 0 && t_build[s].is_stopped()));
+    if (!timers_ok) std::printf("timers: not accumulated\n");
+    return all_equal && timers_ok ? 0 : 3;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "error: %s\n", e.what());
     return 1;

@@ -3,6 +3,8 @@
 // oracle without a GPU.  Not part of the product.
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../compressor-mpc_amd/csrc/qp_solver.h"
 
 template <int N, int NU>
@@ -43,14 +45,19 @@ extern "C" int qp_host_solve(int n, int nu, const double* H, const double* g, co
 // the iterate kernel keeps it: H, f, G (n x nvo row-major), d (K x nvo).
 // Outputs per iteration k: x[k*n..], st[k], nchg[k], ws_out[k], trace[k*16..],
 // ntrace[k].
-template <int N, int NU, int NVO>
+template <int N, int NU, int NVO, bool LDS_HINV = false>
 static void run_map(const double* Hp, const double* fp, const double* Gp, const double* dp, int K,
                     const double* lb, const double* ub, const double* lbA, const double* ubA,
                     uint32_t ws_in, int max_chg, double* xo, int32_t* st, int32_t* nchg, uint32_t* ws_out,
                     uint8_t* trace, int32_t* ntrace) {
   constexpr int NVOA = JMap<N, NVO>::NVOA;
   double H[N][N], f[N];
-  Qp<N, NU> qp;
+  // H^-1 in registers, or (LDS_HINV) as the iterate kernel keeps it: the
+  // upper triangle in a strided array read by columns
+  using HS = std::conditional_t<LDS_HINV, HinvStrided<N, 3>, HinvRegs<N>>;
+  double hbuf[N * N * 3];
+  Qp<N, NU, N, HS> qp;
+  if constexpr (LDS_HINV) qp.Hinv.p = hbuf;
   for (int a = 0; a < N; ++a) {
     for (int b = 0; b < N; ++b) H[a][b] = Hp[a * N + b];
     f[a] = fp[a];
@@ -85,6 +92,8 @@ extern "C" int qp_host_jacobi(int n, int nu, int nvo, const double* H, const dou
                               int32_t* nchg, uint32_t* ws_out, uint8_t* trace, int32_t* ntrace) {
   if (n == 4 && nu == 2 && nvo == 4)
     run_map<4, 2, 4>(H, f, G, d, K, lb, ub, lbA, ubA, ws_in, max_chg, x, st, nchg, ws_out, trace, ntrace);
+  else if (n == 4 && nu == 2 && nvo == -4)  // H^-1 stored as the iterate kernel's LDS copy
+    run_map<4, 2, 4, true>(H, f, G, d, K, lb, ub, lbA, ubA, ws_in, max_chg, x, st, nchg, ws_out, trace, ntrace);
   else if (n == 6 && nu == 2 && nvo == 6)
     run_map<6, 2, 6>(H, f, G, d, K, lb, ub, lbA, ubA, ws_in, max_chg, x, st, nchg, ws_out, trace, ntrace);
   else if (n == 8 && nu == 4 && nvo == 0)

@@ -190,15 +190,18 @@ def test_abi_refuses_coupled_reads_beyond_the_callers_buffers():
 
 # ---- GPU: the product kernel -----------------------------------------------
 
-def product_rank(rank, world, group_gather=None):
+def product_rank(rank, world, group_gather=None, S_total=S_TOTAL, Bn=B):
     import torch
     import cmpc
     from cmpc.coupled import CoupledRank
-    cfg, arr, H, f, G, u_old = problem()
-    sl = S_TOTAL // world
-    glob = [b * S_TOTAL + rank * sl + i for b in range(B) for i in range(sl)]
+    from cmpc.configs import reference_setup
     from cmpc.synthetic import synthetic_batch
-    lin, _, _, _ = synthetic_batch(cfg, B * S_TOTAL // cfg.S, seed=12)
+    # the inputs of problem() (its oracle QPs are not needed here)
+    cfg = cmpc.reference_config("par", "coop", p=20)
+    arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+    lin, u_old, _, _ = synthetic_batch(cfg, Bn * S_total // cfg.S, seed=12)
+    sl = S_total // world
+    glob = [b * S_total + rank * sl + i for b in range(Bn) for i in range(sl)]
     ctx = cmpc.Context(cfg, len(glob) // cfg.S, device=0)
     ctx.configure(arr)
     ctx.set_state(np.ascontiguousarray(u_old[glob]), np.zeros((len(glob), cfg.nV)),
@@ -206,8 +209,8 @@ def product_rank(rank, world, group_gather=None):
     ctx.upload_lin(np.ascontiguousarray(lin[glob]))
     ctx.build()
     Hd, fd, Gd = ctx.download_qp()
-    Gx = torch.from_numpy(synthetic_g_ext(Gd, S_TOTAL, sl, rank * sl)).cuda()
-    cr = CoupledRank(ctx, S_TOTAL, sl, rank, world, Gx)
+    Gx = torch.from_numpy(synthetic_g_ext(Gd, S_total, sl, rank * sl)).cuda()
+    cr = CoupledRank(ctx, S_total, sl, rank, world, Gx)
     cr.step(K)
     torch.cuda.synchronize()
     return cfg, arr, ctx, cr, Hd, fd, Gd, u_old[glob]
@@ -227,14 +230,14 @@ def test_gpu_coupled_kernel_equals_oracle_loop():
     assert np.array_equal(du_gpu, ref)
 
 
-def _gpu_worker(rank, world, port, q):
+def _gpu_worker(rank, world, port, q, S_total=S_TOTAL, Bn=B):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _, _, ctx, cr, *_ = product_rank(rank, world)
+        _, _, ctx, cr, *_ = product_rank(rank, world, S_total=S_total, Bn=Bn)
         parts = [torch.zeros(cr.du_local.shape, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(parts, cr.du_local.cpu())
         if rank == 0:
@@ -263,6 +266,35 @@ def test_gpu_coupled_two_ranks_equal_one():
     sl = S_TOTAL // world
     got = got.reshape(world, B, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
     assert np.array_equal(got, one)
+
+
+@pytest.mark.gpu
+def test_gpu_coupled_config4_partition_eight_ranks_equal_one():
+    """SURVEY config 4's own partition through the product kernel: 8 gloo
+    ranks on the one GPU, each a CoupledRank with S_local = 8 of S_total = 64
+    sub-controllers (s_offset = 8 r: every rank offset 0 ... 56, rank-major
+    plan indexing over 8 ranks in cmpc_coupled_iterate), 256 scenarios, the
+    plans all-gathered once per Jacobi iteration (the exchange that replaces
+    include/nerve_center.h:280-285): bit-exact with one process running all
+    64 sub-controllers."""
+    world, S_total, Bn = 8, 64, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, S_total, Bn)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=600)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    *_, ctx1, cr1, _, _, _, _ = product_rank(0, 1, S_total=S_total, Bn=Bn)
+    one = cr1.du_local.cpu().numpy()
+    ctx1.close()
+    sl = S_total // world
+    got = got.reshape(world, Bn, sl, 4).transpose(1, 0, 2, 3).reshape(-1, 4)
+    assert np.array_equal(got, one)
+    assert np.abs(one).max() > 0
 
 
 @pytest.mark.gpu

@@ -203,7 +203,8 @@ def test_controller_loop_builds_and_fails_loudly_without_device(tmp_path):
 def test_gpu_distributed_controller_api_matches_nerve_center(name, tmp_path):
     """The per-object DistributedController API (Initialize, SetWeights,
     SetOutputReference, GenerateInitialQP, GetInput, UpdateU,
-    GetStateEstimate; distributed_controller.h:131-191), each sub-controller
+    GetStateEstimate; distributed_controller.h:131-191; on odd steps their
+    timed overloads, :155-183), each sub-controller
     on its own one-slot context and the Jacobi loop run on the host as
     NerveCenter runs it, equals cmpc::NerveCenter bit for bit over 6 steps
     with a moving measured output (applied inputs, plans, statuses, state
@@ -217,3 +218,8 @@ def test_gpu_distributed_controller_api_matches_nerve_center(name, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("step ")]
     assert len(lines) == 6 and all(" equal " in l for l in lines), r.stdout
+    # steps 1, 3, 5 ran through the timed overloads (UpdateU / GenerateInitialQP
+    # / GetInput on a CpuTimer, distributed_controller.h:155-183): the same
+    # bits, and the timers accumulated
+    assert sum("(timed overloads)" in l for l in lines) == 3, r.stdout
+    assert "timed overloads: GenerateInitialQP" in r.stdout and "timers: not accumulated" not in r.stdout

@@ -325,7 +325,7 @@ def compare_step(B, S, K, dev, orc, margin, excused):
     return diff & ~flag & ~excused, diff & (flag | excused)
 
 
-def _step_parity(cfg, setup, K, B=96, seed=100):
+def _step_parity(cfg, setup, K, B=96, seed=100, expect_fused=None, threads=1):
     """Three closed-loop steps (state persists: ws, du_old, u_old with the
     first move applied), device and oracle each on their own state: plans
     within tolerance, statuses, nWSR, working sets and the working-set change
@@ -347,13 +347,15 @@ def _step_parity(cfg, setup, K, B=96, seed=100):
                 ctx.iterate(K, flags)
             else:
                 ctx.step(K, flags)
+                if expect_fused is not None:
+                    assert ctx.last_step_fused() == expect_fused, step
             du, st, nw = ctx.download()
             tr, ntr = ctx.download_trace(K)
             u_g, du_g, ws_g = ctx.get_state()
             margin = np.zeros(nq)
             odu, ost, onw, otr, ontr = O.step(dims, arr, lin, K, o_u, o_du, o_ws,
                                               flags=cmpc.CMPC_APPLY_MOVE, init=(step == 0),
-                                              want_trace=True, margin=margin)
+                                              want_trace=True, margin=margin, threads=threads)
             bad, flagged = compare_step(B, cfg.S, K, (du, st, nw, ws_g, tr, ntr),
                                         (odu, ost, onw, o_ws, otr, ontr), margin, excused)
             print(f"step {step}: scenarios differing at a flagged near-tie {flagged.sum()}, "
@@ -373,6 +375,19 @@ def test_gpu_step_matches_oracle(plant, ctype, p, K):
     """_step_parity on the reference plants' configurations."""
     _, setup, _, _ = setup_for(plant, ctype)
     _step_parity(cmpc.reference_config(plant, ctype, p=p), setup, K, seed=100 + p)
+
+
+@pytest.mark.parametrize("plant,ctype,p,K,B", [("par", "cent", 200, 1, 1024),   # SURVEY config 5
+                                              ("par", "coop", 50, 9, 1)])      # the B = 1 call
+def test_gpu_fused_step_matches_oracle(plant, ctype, p, K, B):
+    """_step_parity through the fused one-launch steps CMPC_STEP_AUTO runs at
+    these sizes (config 5: the one-QP-per-wave build with the row solver in
+    the same kernel; B = 1 coop-par: the fused step), each step after the
+    first checked to have run fused, directly against the oracle over three
+    steps with the move applied."""
+    _, setup, _, _ = setup_for(plant, ctype)
+    _step_parity(cmpc.reference_config(plant, ctype, p=p), setup, K, B=B, seed=300 + p, expect_fused=1,
+                 threads=8)
 
 
 # other delays and move counts: m = 1 (nV = nu) and m = 3 (the one-QP-per-wave
@@ -418,6 +433,8 @@ def test_gpu_step_matches_oracle_headline_size():
                 ctx.iterate(K, flags)
             else:
                 ctx.step(K, flags)
+                if expect_fused is not None:
+                    assert ctx.last_step_fused() == expect_fused, step
             du, st, nw = ctx.download()
             tr, ntr = ctx.download_trace(K)
             u_g, du_g, ws_g = ctx.get_state()

@@ -362,6 +362,8 @@ def test_gpu_closed_loop_observer_matches_oracle():
     ("par", "coop", 20, 13, 9),    # a partial last workgroup
     ("par", "ncoop", 50, 3, 9),
     ("par", "cent", 20, 5, 3),     # row solver of each wave
+    ("par", "cent", 20, 3, 3),     # one workgroup, waves 1-2 store results (polled path)
+    ("ser", "cent", 100, 4, 1),    # one workgroup, waves 1-3 store results (polled path)
     ("ser", "cent", 100, 1, 1),    # SURVEY config 1 at B = 1
     ("ser", "coop", 50, 2, 9)])
 def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):

@@ -78,14 +78,14 @@ def test_host_solver_bitexact_vs_oracle(n, nu):
     assert stats["active"] > 1000 and stats.get(0, 0) > 1000
 
 
-def host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg=10):
+def host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg=10, lds_hinv=False):
     n, K = len(f), D.shape[0]
     nvo = D.shape[1]
     x = np.zeros((K, n))
     st = np.zeros(K, np.int32); nchg = np.zeros(K, np.int32); ws = np.zeros(K, np.uint32)
     ntr = np.zeros(K, np.int32); tr = np.zeros((K, 16), np.uint8)
     P = ctypes.POINTER
-    rc = lib.qp_host_jacobi(n, nu, nvo, d(H), d(f), d(G if nvo else np.zeros(1)), d(D if nvo else np.zeros(1)), K,
+    rc = lib.qp_host_jacobi(n, nu, -nvo if lds_hinv else nvo, d(H), d(f), d(G if nvo else np.zeros(1)), d(D if nvo else np.zeros(1)), K,
                             d(lb), d(ub), d(lbA), d(ubA), ctypes.c_uint32(ws_in), max_chg,
                             x.ctypes.data_as(P(ctypes.c_double)), st.ctypes.data_as(P(ctypes.c_int32)),
                             nchg.ctypes.data_as(P(ctypes.c_int32)), ws.ctypes.data_as(P(ctypes.c_uint32)),
@@ -94,15 +94,16 @@ def host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg=10):
     return x, st, nchg, ws, tr, ntr
 
 
-@pytest.mark.parametrize("n,nu,nvo", [(4, 2, 4), (6, 2, 6), (8, 4, 0)])
-def test_host_jacobi_map_form_bitexact_vs_oracle(n, nu, nvo):
+@pytest.mark.parametrize("n,nu,nvo,lds", [(4, 2, 4, False), (4, 2, 4, True), (6, 2, 6, False), (8, 4, 0, False)])
+def test_host_jacobi_map_form_bitexact_vs_oracle(n, nu, nvo, lds):
     """The map form of the Jacobi iterations (qp_solve_map: the map of a
     working set kept across the iterations, rebuilt on a change, the factor
     restored after a solve that left it) against the oracle's stateless
     or_qp_solve_map, iteration by iteration: bit-exact x, status, changes,
     working set and change sequence.  The plans d mostly stay close (the map
     is reused) and sometimes jump (working sets change, drops and adds in
-    phase A and B, returns to an earlier working set)."""
+    phase A and B, returns to an earlier working set).  lds: H^-1 stored as
+    the iterate kernel keeps it (upper triangle, read by columns)."""
     lib = host()
     rng = np.random.default_rng(77 + n)
     stats = {"hit": 0, "chg": 0}
@@ -120,7 +121,7 @@ def test_host_jacobi_map_form_bitexact_vs_oracle(n, nu, nvo):
             for j in rng.choice(2 * n, size=rng.integers(0, n + 1), replace=False):
                 ws_in |= (1 << int(j)) | ((int(rng.integers(0, 2)) << (16 + int(j))))
         max_chg = 10 if trial % 5 else int(rng.integers(0, 4))
-        xh, st, nchg, ws, tr, ntr = host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg)
+        xh, st, nchg, ws, tr, ntr = host_jacobi(lib, H, f, G, D, lb, ub, lbA, ubA, nu, ws_in, max_chg, lds)
         w = ws_in
         for k in range(K):
             xo, info = O.qp_solve_map(H, f, G, D[k], lb, ub, lbA, ubA, nu, w, max_chg=max_chg)
