@@ -660,6 +660,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
     // SURVEY config 2, tools/time_small.py.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     constexpr int NVO = M * (NUT - NU);
+    constexpr int NVOA = NVO > 0 ? NVO : 1;
     const int gi = g_first + (lane >> 2) * nwaves;
     if (gi < ngroups) {
       const int ql = 4 * gi + (lane & 3);
@@ -667,7 +668,15 @@ void cmpc_build_rows_kernel(BuildParams P) {
       const int qc = al ? ql : nqp - 1;
       const int sl = qc & (S - 1);
       const double* qr = P.qp + (size_t)qc * P.qp_len;
-      lane_solve_qp<NV, NU, NVO, FUSE == 4, false, 1>(P.sv, qc, al, sl, lane - sl, qr, qr + NV * NV + NV);
+      // G of the lane's QP into the wave's own LDS region (free once its
+      // groups are built; the launcher checks its size), lane-contiguous, where
+      // the map form replaces it by U = H^-1 G (registers: the solve's map)
+      double* gl = wreg + lane;
+#pragma unroll
+      for (int a = 0; a < NV; ++a)
+#pragma unroll
+        for (int c = 0; c < NVOA; ++c) gl[(a * NVOA + c) * 64] = NVO > 0 ? qr[NV * NV + NV + a * NVO + c] : 0.0;
+      lane_solve_qp<NV, NU, NVO, FUSE == 4, false, 64>(P.sv, qc, al, sl, lane - sl, qr, gl);
     }
   }
 #if CMPC_ROWS_TIMING
@@ -709,6 +718,9 @@ static int rows_launch(const BuildParams& P, hipStream_t s) {
   per_cu = std::max(1, std::min(per_cu, cmpc_rows_resident_groups(P.rows, WPG)));
   const int need = std::max(1, ((P.nqp + 3) / 4 + WPG - 1) / WPG);
   const int grid = std::max(1, std::min(need, P.cus * per_cu));
+  // the lane solver after the groups (FUSE 3/4) solves one QP per lane: every
+  // wave's groups must fit its 64 lanes (16 groups of four QPs)
+  if (FUSE >= 3 && ((P.nqp + 3) / 4 + grid * WPG - 1) / (grid * WPG) > 16) return -1;
   cmpc_launch(kern, dim3(grid), dim3(64 * WPG), lds, s, P);
   return 0;
 }

@@ -25,7 +25,10 @@
 #define ROWS_FUSED_LANE_CASE(NS_, NY_, NU_, M_)                                       \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) { \
     if (cmpc_rows_waves_per_group(P.rows) != 4 || ring) return -1;                   \
-    if ((P.nqp + 3) / 4 > 16 * 4 * P.cus) return -1;                                 \
+    if (P.rows.per_wave < (NU_ * M_) * (NU_ * M_) * 64) return -1; /* G / U columns */ \
+    /* one QP per lane: at most 16 groups per wave of the launch's 2 (WPE 2) */      \
+    /* 4-wave workgroups per CU, fewer if the LDS layout allows fewer */            \
+    if ((P.nqp + 3) / 4 > 16 * 4 * P.cus * std::min(2, cmpc_rows_resident_groups(P.rows, 4))) return -1; \
     *solver = CMPC_SOLVE_LANE;                                                         \
     if (trace) return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 4>(P, s);           \
     return rows_launch<NS_, NY_, NU_, M_, 4, false, 2, 3>(P, s);                      \
