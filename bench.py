@@ -233,12 +233,14 @@ def traced_changes(ctx, K, bind, steps):
     return float(np.mean(tot)), tot
 
 
-def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2, seed=4000):
+def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2, seed=4000, markers=False):
     """One SURVEY §8(d) configuration on this GPU: NB resident batches of B
     scenarios, each with its own controller state, step i on batch i % NB
     (build + K Jacobi iterations, first move applied: cmpc_step, fused into
     one launch where CMPC_STEP_AUTO picks that); then the build kernel alone
-    with events for its roofline fraction."""
+    with events for its roofline fraction.  markers: a torch.cuda._sleep
+    launch before and after the event-timed pass, so that a kernel trace of
+    the run can be cut to that pass (tools/configs_pass_stats.py)."""
     import torch
     import cmpc
     from cmpc.configs import reference_setup
@@ -310,10 +312,14 @@ def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2,
         dt_sync = (time.perf_counter() - t0) / steps
         # device time of the step's kernels (events), then the build alone
         restore()
+        if markers:
+            torch.cuda._sleep(1000)
         ctx.enable_timing(True)
         for k in range(steps):
             bind(i + k)
             ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+        if markers:
+            torch.cuda._sleep(1000)
         kt = {}
         for kn, kid in (("build", cmpc.CMPC_KERNEL_BUILD), ("iterate", cmpc.CMPC_KERNEL_ITERATE),
                         ("fused_step", cmpc.CMPC_KERNEL_STEP)):
@@ -419,7 +425,7 @@ def recorded_run_changes(local, n_steps=10000):
                     "headline's working_set_changes_per_qp_step is the same quantity)"}
 
 
-def run_configs(local, settle_seconds, steps, with_cpp=True):
+def run_configs(local, settle_seconds, steps, with_cpp=True, markers=False):
     """SURVEY §8(d) / BASELINE.json configs 2, 3 and 5 at their batch sizes on
     this GPU, and (with_cpp) config 1 and the coop-par B = 1 step through the
     C++ adapter; each entry failure-tolerant."""
@@ -428,7 +434,8 @@ def run_configs(local, settle_seconds, steps, with_cpp=True):
                                      "3": ("par", "ncoop", 50, 65536, 1),
                                      "5": ("par", "cent", 200, 1024, 1)}.items():
         try:
-            configs[key] = time_config(key, pl, ct, p_, B_, K_, local, settle_seconds, max(20, steps))
+            configs[key] = time_config(key, pl, ct, p_, B_, K_, local, settle_seconds, max(20, steps),
+                                       markers=markers)
         except Exception as e:  # reported, never required
             log(f"config {key} failed: {e}")
             configs[key] = {"error": str(e)[:300]}
@@ -498,7 +505,8 @@ def main():
             dist.init_process_group("gloo")
 
     if args.configs_only:
-        print(json.dumps({"configs": run_configs(local, args.settle_seconds, args.steps, with_cpp=False)}),
+        print(json.dumps({"configs": run_configs(local, args.settle_seconds, args.steps, with_cpp=False,
+                                                 markers=True)}),
               flush=True)
         return
 

@@ -204,6 +204,9 @@ def product_rank(rank, world, group_gather=None, S_total=S_TOTAL, Bn=B):
     glob = [b * S_total + rank * sl + i for b in range(Bn) for i in range(sl)]
     ctx = cmpc.Context(cfg, len(glob) // cfg.S, device=0)
     ctx.configure(arr)
+    # one build kernel for every sharding: AUTO picks by batch size, and the
+    # two kernels agree to 1e-11, not bit for bit (test_gpu_parity.py)
+    ctx.set_build_variant(cmpc.CMPC_BUILD_ROWS)
     ctx.set_state(np.ascontiguousarray(u_old[glob]), np.zeros((len(glob), cfg.nV)),
                   np.zeros(len(glob), np.uint32))
     ctx.upload_lin(np.ascontiguousarray(lin[glob]))

@@ -433,8 +433,6 @@ def test_gpu_step_matches_oracle_headline_size():
                 ctx.iterate(K, flags)
             else:
                 ctx.step(K, flags)
-                if expect_fused is not None:
-                    assert ctx.last_step_fused() == expect_fused, step
             du, st, nw = ctx.download()
             tr, ntr = ctx.download_trace(K)
             u_g, du_g, ws_g = ctx.get_state()
