@@ -17,7 +17,8 @@
 
 // ---------------------------------------------------------------------------
 // Warm-started dual active-set QP solver (lane per QP).  Same specification
-// and arithmetic order as oracle/or_qp.c; see DESIGN.md §QP.
+// and arithmetic order as oracle/or_qp.c (version 4: every accumulation
+// c +- a b is one fma, here and in the oracle); see DESIGN.md §4.
 // ---------------------------------------------------------------------------
 #ifndef CMPC_QP_ABL
 #define CMPC_QP_ABL 0  // timing-only ablations (results invalid): 1 no phase B, 2 no phase A solve
@@ -222,7 +223,7 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D
     if (j < K) {
       double d = M[j][j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
+      for (int k = 0; k < j; ++k) d = fma(-(L[j][k] * L[j][k]), D[k], d);
       ok = ok && (d > rel * M[j][j]);
       D[j] = d;
       const double r = 1.0 / d;
@@ -233,7 +234,7 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D
         if (i < K) {
           double sacc = M[i][j];
 #pragma unroll
-          for (int k = 0; k < j; ++k) sacc = sacc - (L[i][k] * L[j][k]) * D[k];
+          for (int k = 0; k < j; ++k) sacc = fma(-(L[i][k] * L[j][k]), D[k], sacc);
           L[i][j] = sacc * r;
         }
       }
@@ -258,7 +259,7 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
     if (i < K) {
       double v = b[i];
 #pragma unroll
-      for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
+      for (int k = 0; k < i; ++k) v = fma(-L[i][k], y[k], v);
       y[i] = v;
       zz[i] = v * R[i];
     }
@@ -269,7 +270,7 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
       double v = zz[i];
 #pragma unroll
       for (int k = i + 1; k < N; ++k)
-        if (k < K) v = v - L[k][i] * x[k];
+        if (k < K) v = fma(-L[k][i], x[k], v);
       x[i] = v;
     } else {
       x[i] = 0.0;
@@ -329,7 +330,7 @@ CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
     if (j > a && j < W.K) {
       const double p = w[j];
       const double t = alpha * p;
-      const double d = W.D[j] + t * p;
+      const double d = fma(t, p, W.D[j]);
       const double r = 1.0 / d;
       const double bt = t * r;
       alpha = alpha * (W.D[j] * r);
@@ -338,8 +339,8 @@ CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
 #pragma unroll
       for (int i = j + 1; i < N; ++i)
         if (i < W.K) {
-          w[i] = w[i] - p * W.L[i][j];
-          W.L[i][j] = W.L[i][j] + bt * w[i];
+          w[i] = fma(-p, W.L[i][j], w[i]);
+          W.L[i][j] = fma(bt, w[i], W.L[i][j]);
         }
     }
   }
@@ -479,7 +480,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
   for (int i = 0; i < N; ++i) {
     double sacc = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + q.Hinv(i, j) * g[j];
+    for (int j = 0; j < N; ++j) sacc = fma(q.Hinv(i, j), g[j], sacc);
     xu[i] = -sacc;
   }
   // A. warm start: slot a = the a-th active constraint of ws_in in ascending
@@ -533,7 +534,7 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
         double ha[N];
         wset_h(q, W, a, ha);
 #pragma unroll
-        for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
+        for (int r = 0; r < N; ++r) x[r] = fma(W.lam[a], ha[r], x[r]);
       }
     }
   }
@@ -602,7 +603,7 @@ CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[
           double ha[N];
           wset_h(q, W, a, ha);
 #pragma unroll
-          for (int r = 0; r < N; ++r) z[r] = z[r] - rv[a] * ha[r];
+          for (int r = 0; r < N; ++r) z[r] = fma(-rv[a], ha[r], z[r]);
         }
       }
       const double zn = q.nu_dot(pj, ps, z);
@@ -626,7 +627,7 @@ CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[
         }
 #pragma unroll
         for (int a = 0; a < N; ++a)
-          if (a < W.K) W.lam[a] = W.lam[a] - t1 * rv[a];
+          if (a < W.K) W.lam[a] = fma(-t1, rv[a], W.lam[a]);
         up = up + t1;
         int kj = 0, ks = 0;
 #pragma unroll
@@ -650,10 +651,10 @@ CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[
       const bool full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
 #pragma unroll
-      for (int r = 0; r < N; ++r) x[r] = x[r] + t * z[r];
+      for (int r = 0; r < N; ++r) x[r] = fma(t, z[r], x[r]);
 #pragma unroll
       for (int a = 0; a < N; ++a)
-        if (a < W.K) W.lam[a] = W.lam[a] - t * rv[a];
+        if (a < W.K) W.lam[a] = fma(-t, rv[a], W.lam[a]);
       up = up + t;
       if (full) {
         if (TRACE) trace_push(o, 1, pj, ps);
@@ -794,9 +795,9 @@ CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const 
       wset_h(q, W, a, ha);
 #pragma unroll
       for (int r = 0; r < N; ++r) {
-        mp.x0[r] = mp.x0[r] + mp.lam0[a] * ha[r];
+        mp.x0[r] = fma(mp.lam0[a], ha[r], mp.x0[r]);
 #pragma unroll
-        for (int c = 0; c < NVO; ++c) mp.X[r][c] = mp.X[r][c] + mp.Lam[a][c] * ha[r];
+        for (int c = 0; c < NVO; ++c) mp.X[r][c] = fma(mp.Lam[a][c], ha[r], mp.X[r][c]);
       }
     }
   }
@@ -858,7 +859,7 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
     for (int a = 0; a < N; ++a) {
       double v = mp.lam0[a];
 #pragma unroll
-      for (int c = 0; c < NVO; ++c) v = v + mp.Lam[a][c] * d[c];
+      for (int c = 0; c < NVO; ++c) v = fma(mp.Lam[a][c], d[c], v);
       lam[a] = v;
       if (a < mp.K && v < wv) {
         wv = v;
@@ -874,7 +875,7 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
     for (int r = 0; r < N; ++r) {
       double v = mp.x0[r];
 #pragma unroll
-      for (int c = 0; c < NVO; ++c) v = v + mp.X[r][c] * d[c];
+      for (int c = 0; c < NVO; ++c) v = fma(mp.X[r][c], d[c], v);
       x[r] = v;
     }
     bool anyv = false;
@@ -919,7 +920,7 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
     for (int r = 0; r < N; ++r) {
       double v = xu0[r];
 #pragma unroll
-      for (int c = 0; c < NVO; ++c) v = v - U(r, c) * d[c];
+      for (int c = 0; c < NVO; ++c) v = fma(-U(r, c), d[c], v);
       xu[r] = v;
     }
     for (int it = 0; it <= N && !done; ++it) {
@@ -966,7 +967,7 @@ CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, con
           double ha[N];
           wset_h(q, W, a, ha);
 #pragma unroll
-          for (int r = 0; r < N; ++r) x[r] = x[r] + W.lam[a] * ha[r];
+          for (int r = 0; r < N; ++r) x[r] = fma(W.lam[a], ha[r], x[r]);
         }
       }
     }
@@ -984,7 +985,7 @@ CMPC_HD void jmap_terms(const HS& Hinv, const double (&f)[N], double* gb, double
   for (int i = 0; i < N; ++i) {
     double sacc = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + Hinv(i, j) * f[j];
+    for (int j = 0; j < N; ++j) sacc = fma(Hinv(i, j), f[j], sacc);
     xu0[i] = -sacc;
   }
 #pragma unroll
@@ -996,7 +997,7 @@ CMPC_HD void jmap_terms(const HS& Hinv, const double (&f)[N], double* gb, double
     for (int i = 0; i < N; ++i) {
       double u = 0.0;
 #pragma unroll
-      for (int j = 0; j < N; ++j) u = u + Hinv(i, j) * gc[j];
+      for (int j = 0; j < N; ++j) u = fma(Hinv(i, j), gc[j], u);
       gb[(i * NVOA + c) * GSTRIDE] = u;
     }
   }
@@ -1011,14 +1012,14 @@ CMPC_HD void jmap_terms(const HS& Hinv, const double (&f)[N], const double* gb, 
   for (int i = 0; i < N; ++i) {
     double sacc = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + Hinv(i, j) * f[j];
+    for (int j = 0; j < N; ++j) sacc = fma(Hinv(i, j), f[j], sacc);
     xu0[i] = -sacc;
 #pragma unroll
     for (int c = 0; c < NVOA; ++c) {
       double u = 0.0;
       if (c < NVO) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) u = u + Hinv(i, j) * gb[(j * NVOA + c) * GSTRIDE];
+        for (int j = 0; j < N; ++j) u = fma(Hinv(i, j), gb[(j * NVOA + c) * GSTRIDE], u);
       }
       U[i][c] = u;
     }

@@ -87,7 +87,7 @@ __device__ __forceinline__ bool hinv_row(const double (&Hl)[N], int l, double (&
     double d = rbc<j>(Hl[j]);
 #pragma unroll
     for (int k = 0; k < N; ++k)
-      if (k < j) d = d - (Lf[j][k] * Lf[j][k]) * D[k];
+      if (k < j) d = fma(-(Lf[j][k] * Lf[j][k]), D[k], d);
     ok = ok && (d > 0.0);
     D[j] = d;
     R[j] = 1.0 / d;
@@ -95,7 +95,7 @@ __device__ __forceinline__ bool hinv_row(const double (&Hl)[N], int l, double (&
     double sacc = Hl[j];  // M[i][j] of lane i
 #pragma unroll
     for (int k = 0; k < N; ++k)
-      if (k < j) sacc = sacc - (Li[k] * Lf[j][k]) * D[k];
+      if (k < j) sacc = fma(-(Li[k] * Lf[j][k]), D[k], sacc);
     if (l > j) Li[j] = sacc * R[j];
   });
   // column l of H^-1 (ldl_solve_k(N, L, R, e_l)): entries i <= l are H^-1(i, l)
@@ -167,7 +167,7 @@ __device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowb
       double d = nval<N, NU>(hv[j], rowbase, W.j[j], W.side[j]);
       const double mjj = d;
 #pragma unroll
-      for (int k = 0; k < j; ++k) d = d - (W.L[j][k] * W.L[j][k]) * W.D[k];
+      for (int k = 0; k < j; ++k) d = fma(-(W.L[j][k] * W.L[j][k]), W.D[k], d);
       ok = ok && (d > TOL_Z * mjj);
       W.D[j] = d;
       const double r = 1.0 / d;
@@ -178,7 +178,7 @@ __device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowb
         if (i < W.K) {
           double sacc = nval<N, NU>(hv[i], rowbase, W.j[j], W.side[j]);
 #pragma unroll
-          for (int k = 0; k < j; ++k) sacc = sacc - (W.L[i][k] * W.L[j][k]) * W.D[k];
+          for (int k = 0; k < j; ++k) sacc = fma(-(W.L[i][k] * W.L[j][k]), W.D[k], sacc);
           W.L[i][j] = sacc * r;
         }
       }
@@ -267,7 +267,7 @@ __device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const doub
       double z_l = hp_l;
 #pragma unroll
       for (int a = 0; a < N; ++a)
-        if (a < W.K) z_l = z_l - rv[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+        if (a < W.K) z_l = fma(-rv[a], hval<N, NU>(t, l, W.j[a], W.side[a]), z_l);
       const double zn = nval<N, NU>(z_l, rowbase, pj, ps);
       const double den = nval<N, NU>(hp_l, rowbase, pj, ps);
       int k = -1;
@@ -289,7 +289,7 @@ __device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const doub
         }
 #pragma unroll
         for (int a = 0; a < N; ++a)
-          if (a < W.K) W.lam[a] = W.lam[a] - t1 * rv[a];
+          if (a < W.K) W.lam[a] = fma(-t1, rv[a], W.lam[a]);
         up = up + t1;
         int kj = 0, ks = 0;
 #pragma unroll
@@ -312,10 +312,10 @@ __device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const doub
       const double t2 = -sl * rzn;
       const bool full = (k < 0) || (t2 <= t1);
       const double tt = full ? t2 : t1;
-      x_l = x_l + tt * z_l;
+      x_l = fma(tt, z_l, x_l);
 #pragma unroll
       for (int a = 0; a < N; ++a)
-        if (a < W.K) W.lam[a] = W.lam[a] - tt * rv[a];
+        if (a < W.K) W.lam[a] = fma(-tt, rv[a], W.lam[a]);
       up = up + tt;
       if (full) {
         if (TRACE) trace_push(o, 1, pj, ps);
@@ -393,7 +393,7 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
     row_gather<N>(g_l, G);
     double sacc = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * G[j];
+    for (int j = 0; j < N; ++j) sacc = fma(hr[j], G[j], sacc);
     xu_l = -sacc;
   }
   // A. warm start: slots in ascending j, the full factor
@@ -450,7 +450,7 @@ __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double
     x_l = xu_l;
 #pragma unroll
     for (int a = 0; a < N; ++a)
-      if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+      if (a < W.K) x_l = fma(W.lam[a], hval<N, NU>(t, l, W.j[a], W.side[a]), x_l);
   }
   qp_row_phase_b<TRACE, N, NU>(q, t, sc, l, rowbase, W, x_l, chg, done, max_chg, o);
 }
@@ -476,7 +476,7 @@ __device__ __forceinline__ void row_jmap_terms(const double (&hr)[N], double f_l
   row_gather<N>(f_l, F);
   double sacc = 0.0;
 #pragma unroll
-  for (int j = 0; j < N; ++j) sacc = sacc + hr[j] * F[j];
+  for (int j = 0; j < N; ++j) sacc = fma(hr[j], F[j], sacc);
   xu0_l = -sacc;
 #pragma unroll
   for (int c = 0; c < RowMap<N, NVO>::NVOA; ++c) U_l[c] = 0.0;
@@ -486,7 +486,7 @@ __device__ __forceinline__ void row_jmap_terms(const double (&hr)[N], double f_l
     row_gather<N>(Gl[c], Gc);
     double u = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) u = u + hr[j] * Gc[j];
+    for (int j = 0; j < N; ++j) u = fma(hr[j], Gc[j], u);
     U_l[c] = u;
   }
 }
@@ -516,9 +516,9 @@ __device__ __forceinline__ void row_jmap_build(const RowQp<N, NU>& q, const doub
   for (int a = 0; a < N; ++a) {
     if (a < W.K) {
       const double h = hval<N, NU>(t, l, W.j[a], W.side[a]);
-      mp.x0_l = mp.x0_l + mp.lam0[a] * h;
+      mp.x0_l = fma(mp.lam0[a], h, mp.x0_l);
 #pragma unroll
-      for (int c = 0; c < NVO; ++c) mp.X_l[c] = mp.X_l[c] + mp.Lam[a][c] * h;
+      for (int c = 0; c < NVO; ++c) mp.X_l[c] = fma(mp.Lam[a][c], h, mp.X_l[c]);
     }
   }
 }
@@ -565,7 +565,7 @@ __device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const do
     for (int a = 0; a < N; ++a) {
       double v = mp.lam0[a];
 #pragma unroll
-      for (int c = 0; c < NVO; ++c) v = v + mp.Lam[a][c] * d[c];
+      for (int c = 0; c < NVO; ++c) v = fma(mp.Lam[a][c], d[c], v);
       lam[a] = v;
       if (a < mp.K && v < wv) {
         wv = v;
@@ -579,7 +579,7 @@ __device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const do
   if (stay) {
     double v = mp.x0_l;
 #pragma unroll
-    for (int c = 0; c < NVO; ++c) v = v + mp.X_l[c] * d[c];
+    for (int c = 0; c < NVO; ++c) v = fma(mp.X_l[c], d[c], v);
     x_l = v;
     int ps = 0;
     if (row_scan<N, NU>(x_l, sc, mp.wc, l, rowbase, ps) < 0) {  // nothing violated: done
@@ -604,7 +604,7 @@ __device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const do
   if (!done && !stay) {
     double xu_l = xu0_l;
 #pragma unroll
-    for (int c = 0; c < NVO; ++c) xu_l = xu_l - U_l[c] * d[c];
+    for (int c = 0; c < NVO; ++c) xu_l = fma(-U_l[c], d[c], xu_l);
     for (int it = 0; it <= N && !done; ++it) {
       if (it > 0) {
         double rhs[N];
@@ -640,7 +640,7 @@ __device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const do
       x_l = xu_l;
 #pragma unroll
       for (int a = 0; a < N; ++a)
-        if (a < W.K) x_l = x_l + W.lam[a] * hval<N, NU>(t, l, W.j[a], W.side[a]);
+        if (a < W.K) x_l = fma(W.lam[a], hval<N, NU>(t, l, W.j[a], W.side[a]), x_l);
     }
   }
   qp_row_phase_b<TRACE, N, NU>(q, t, sc, l, rowbase, W, x_l, chg, done, max_chg, o);

@@ -15,8 +15,12 @@
  * (libs/mpc_qp_solver.cc:66-69), warm start from the previous working set of
  * the same QP slot (hotstart).
  *
- * Algorithm specification, version 3 (the HIP kernels implement the same
- * steps in the same arithmetic order):
+ * Algorithm specification, version 4 (the HIP kernels implement the same
+ * steps in the same arithmetic order).  Version 4: every
+ * accumulation c +- a b below (the factor, its solves and updates, the
+ * products with Hinv, U, the map and the step) is one fused multiply-add,
+ * C99 fma() here and v_fma_f64 on the device (one rounding each; the build is
+ * -ffp-contract=off everywhere else):
  *   0. H = L D L' with reciprocal pivots R = 1/D (any pivot <= 0 -> NOT_PD);
  *      Hinv column by column from that factor.
  *      nall_j = the normal of constraint j without its side: e_j (j < n),
@@ -132,14 +136,14 @@ static int ldl(int n, double M[QMAX][QMAX], double L[QMAX][QMAX], double D[QMAX]
   int rc = 0;
   for (int j = 0; j < n; ++j) {
     double d = M[j][j];
-    for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
+    for (int k = 0; k < j; ++k) d = fma(-(L[j][k] * L[j][k]), D[k], d);
     D[j] = d;
     R[j] = 1.0 / d;
     if (!(d > rel * M[j][j]) && !rc) rc = -(j + 1);
     L[j][j] = 1.0;
     for (int i = j + 1; i < n; ++i) {
       double s = M[i][j];
-      for (int k = 0; k < j; ++k) s = s - (L[i][k] * L[j][k]) * D[k];
+      for (int k = 0; k < j; ++k) s = fma(-(L[i][k] * L[j][k]), D[k], s);
       L[i][j] = s * R[j];
     }
   }
@@ -155,13 +159,13 @@ static void ldl_solve(int n, double L[QMAX][QMAX], const double R[QMAX], const d
   double y[QMAX];
   for (int i = 0; i < n; ++i) {
     double v = b[i];
-    for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) v = fma(-L[i][k], y[k], v);
     y[i] = v;
   }
   for (int i = 0; i < n; ++i) zz[i] = y[i] * R[i];
   for (int i = n - 1; i >= 0; --i) {
     double v = zz[i];
-    for (int k = i + 1; k < n; ++k) v = v - L[k][i] * x[k];
+    for (int k = i + 1; k < n; ++k) v = fma(-L[k][i], x[k], v);
     x[i] = v;
   }
 }
@@ -233,15 +237,15 @@ static void wset_remove(wset_t* W, int a) {
   for (int j = a + 1; j < W->K; ++j) {
     const double p = w[j];
     const double t = alpha * p;
-    const double d = W->D[j] + t * p;
+    const double d = fma(t, p, W->D[j]);
     const double r = 1.0 / d;
     const double bt = t * r;
     alpha = alpha * (W->D[j] * r);
     W->D[j] = d;
     W->R[j] = r;
     for (int i = j + 1; i < W->K; ++i) {
-      w[i] = w[i] - p * W->L[i][j];
-      W->L[i][j] = W->L[i][j] + bt * w[i];
+      w[i] = fma(-p, W->L[i][j], w[i]);
+      W->L[i][j] = fma(bt, w[i], W->L[i][j]);
     }
   }
   for (int i = a; i + 1 < W->K; ++i) {
@@ -315,11 +319,11 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
   double xu0[QMAX], U[QMAX][CMPC_MAX_NVO], g[QMAX];
   for (int i = 0; i < n; ++i) {
     double s = 0;
-    for (int j = 0; j < n; ++j) s = s + q.Hinv[i][j] * f[j];
+    for (int j = 0; j < n; ++j) s = fma(q.Hinv[i][j], f[j], s);
     xu0[i] = -s;
     for (int c = 0; c < nvo; ++c) {
       double u = 0;
-      for (int j = 0; j < n; ++j) u = u + q.Hinv[i][j] * G[j * nvo + c];
+      for (int j = 0; j < n; ++j) u = fma(q.Hinv[i][j], G[j * nvo + c], u);
       U[i][c] = u;
     }
     /* the gradient f + G d: the margin scales only (checker) */
@@ -371,7 +375,7 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
     }
     for (int a = 0; a < W.K; ++a) {
       double v = lam0[a];
-      for (int c = 0; c < nvo; ++c) v = v + Lam[a][c] * d[c];
+      for (int c = 0; c < nvo; ++c) v = fma(Lam[a][c], d[c], v);
       W.lam[a] = v;
     }
     int first = 1, dropped = 0;
@@ -397,7 +401,7 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
       if (!dropped) { /* leaving the map: x_u = x_u0 - U d */
         for (int r = 0; r < n; ++r) {
           double v = xu0[r];
-          for (int c = 0; c < nvo; ++c) v = v - U[r][c] * d[c];
+          for (int c = 0; c < nvo; ++c) v = fma(-U[r][c], d[c], v);
           xu[r] = v;
         }
         dropped = 1;
@@ -419,13 +423,13 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
         double h[QMAX];
         hinv_nu(&q, W.j[a], W.side[a], h);
         for (int r = 0; r < n; ++r) {
-          x0[r] = x0[r] + lam0[a] * h[r];
-          for (int c = 0; c < nvo; ++c) X[r][c] = X[r][c] + Lam[a][c] * h[r];
+          x0[r] = fma(lam0[a], h[r], x0[r]);
+          for (int c = 0; c < nvo; ++c) X[r][c] = fma(Lam[a][c], h[r], X[r][c]);
         }
       }
       for (int r = 0; r < n; ++r) {
         double v = x0[r];
-        for (int c = 0; c < nvo; ++c) v = v + X[r][c] * d[c];
+        for (int c = 0; c < nvo; ++c) v = fma(X[r][c], d[c], v);
         x[r] = v;
       }
     } else {
@@ -433,7 +437,7 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
       for (int a = 0; a < W.K; ++a) {
         double h[QMAX];
         hinv_nu(&q, W.j[a], W.side[a], h);
-        for (int r = 0; r < n; ++r) x[r] = x[r] + W.lam[a] * h[r];
+        for (int r = 0; r < n; ++r) x[r] = fma(W.lam[a], h[r], x[r]);
       }
     }
   }
@@ -477,7 +481,7 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
       for (int a = 0; a < W.K; ++a) {
         double h[QMAX];
         hinv_nu(&q, W.j[a], W.side[a], h);
-        for (int r = 0; r < n; ++r) z[r] = z[r] - rv[a] * h[r];
+        for (int r = 0; r < n; ++r) z[r] = fma(-rv[a], h[r], z[r]);
       }
       const double zn = nu_dot(&q, pj, ps, z);
       const double den = nu_dot(&q, pj, ps, hp);
@@ -504,7 +508,7 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
           status = CMPC_QP_INFEASIBLE;
           goto done;
         }
-        for (int a = 0; a < W.K; ++a) W.lam[a] = W.lam[a] - t1 * rv[a];
+        for (int a = 0; a < W.K; ++a) W.lam[a] = fma(-t1, rv[a], W.lam[a]);
         up = up + t1;
         trace_push(info, 0, W.j[k], W.side[k]);
         wset_remove(&W, k);
@@ -520,8 +524,8 @@ int or_qp_solve_map(int n, int nu, const double* H, const double* f, int nvo,
       if (k >= 0) mg(&q, t2, t1, fmax(fabs(t1), fabs(t2)));
       const int full = (k < 0) || (t2 <= t1);
       const double t = full ? t2 : t1;
-      for (int r = 0; r < n; ++r) x[r] = x[r] + t * z[r];
-      for (int a = 0; a < W.K; ++a) W.lam[a] = W.lam[a] - t * rv[a];
+      for (int r = 0; r < n; ++r) x[r] = fma(t, z[r], x[r]);
+      for (int a = 0; a < W.K; ++a) W.lam[a] = fma(-t, rv[a], W.lam[a]);
       up = up + t;
       if (full) {
         trace_push(info, 1, pj, ps);

@@ -15,7 +15,9 @@ the records, not assumed:
     segment boundary is observed twice (cmpc/driver.py docstring; the
     records printed at 50 and 50.05 s hold the same plant state).
 With both, u(t) and y(t) equal the records to all 6 printed digits at every
-instant.  Comparison: string equality of %.6g; |v| < 1e-12 counts as 0 (the
+instant, but for at most two rounding-boundary ties per run (a value within
+1e-9 of a %.6g boundary, printed as the other neighbour: golden_cases.
+six_digit_rows).  Comparison: %.6g; |v| < 1e-12 counts as 0 (the
 parallel plant's y[2] is a difference of two identical compressors' values,
 0 up to one ulp of cancellation, which the reference prints as 0 or
 2.22045e-16 depending on rounding order)."""
@@ -31,11 +33,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LONG = os.path.join(HERE, "golden", "traj_long.npz")
 TRAJ = {"cent-par": "par_centralized", "coop-par": "par_coop9", "ncoop-par": "par_ncoop9",
         "cent-ser": "ser_centralized", "coop-ser": "ser_coop9", "ncoop-ser": "ser_ncoop9"}
-
-
-def six(a):
-    a = np.asarray(a, dtype=np.float64)
-    return np.array([0.0 if abs(v) < 1e-12 else float("%.6g" % v) for v in a.ravel()]).reshape(a.shape)
 
 
 # ---- CPU: the fixture -----------------------------------------------------------
@@ -73,10 +70,11 @@ def test_oracle_closed_loop_reproduces_reference_run(name, n):
     for k in range(n):
         y[k] = loop.step()
         u[k] = loop.u_ctrl
-    bad_u = np.flatnonzero(np.any(six(u) != six(ur[:n]), axis=1))
-    bad_y = np.flatnonzero(np.any(six(y) != six(yr[:n]), axis=1))
+    bad_u, tie_u = GC.six_digit_rows(u, ur[:n])
+    bad_y, tie_y = GC.six_digit_rows(y, yr[:n])
     assert bad_u.size == 0, ("u differs at records", bad_u[:5])
     assert bad_y.size == 0, ("y differs at records", bad_y[:5])
+    assert tie_u.size + tie_y.size <= 2, (tie_u, tie_y)  # rounding-boundary ties, rare
 
 
 def test_reference_observer_gain_shape():
@@ -132,10 +130,11 @@ def test_gpu_closed_loop_reproduces_reference_run(name):
     u, y = ub.cpu().numpy(), yb.cpu().numpy()
     for b in range(1, B):
         assert np.array_equal(u[:, b], u[:, 0]) and np.array_equal(y[:, b], y[:, 0])
-    bad_u = np.flatnonzero(np.any(six(u[:, 0]) != six(ur), axis=1))
-    bad_y = np.flatnonzero(np.any(six(y[:, 0]) != six(yr), axis=1))
+    bad_u, tie_u = GC.six_digit_rows(u[:, 0], ur)
+    bad_y, tie_y = GC.six_digit_rows(y[:, 0], yr)
     assert bad_u.size == 0, ("u differs at records", bad_u[:5], u[bad_u[:2], 0], ur[bad_u[:2]])
     assert bad_y.size == 0, ("y differs at records", bad_y[:5], y[bad_y[:2], 0], yr[bad_y[:2]])
+    assert tie_u.size + tie_y.size <= 2, (tie_u, tie_y)  # rounding-boundary ties, rare
 
 
 @pytest.mark.gpu

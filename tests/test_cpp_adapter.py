@@ -149,14 +149,17 @@ def test_gpu_cpp_harness_writes_reference_run(name, tmp_path):
     gold = np.load(os.path.join(HERE, "golden", "traj_long.npz"))
     ur, yr = gold[f"{plant}_{key}_u"], gold[f"{plant}_{key}_y"]
     assert len(recs) == len(ur) == 10000
-    six = lambda vals: ["0" if abs(float(v)) < 1e-12 else "%.6g" % float(v) for v in vals]
     first = json.load(open(os.path.join(HERE, "golden", f"traj_{plant}_{key}.json")))["records"]
+    ties = 0
     for k, rec in enumerate(recs):
         assert float(rec["t"]) == float("%g" % (k * 0.05)), (k, rec["t"])
-        assert six(rec["u"].split()) == six(ur[k]), (k, rec["u"], ur[k])
-        assert six(rec["y"].split()) == six(yr[k]), (k, rec["y"], yr[k])
+        for key_, ref in (("u", ur[k]), ("y", yr[k])):
+            eq, tie = GC.six_digit_strings_ok(rec[key_].split(), ref)
+            assert eq or tie, (k, key_, rec[key_], ref)
+            ties += tie
         if k < len(first):
             assert [float(v) for v in rec["x"].split()] == first[k]["x"], k
+    assert ties <= 2, ties  # rounding-boundary ties (golden_cases.six_digit_rows)
 
 
 @pytest.mark.gpu
@@ -177,10 +180,13 @@ def test_gpu_cpp_harness_timed_prefix_keeps_trajectory(n_timing, tmp_path):
     recs = read_dat(tmp_path / "parallel" / "out.dat")
     gold = np.load(os.path.join(HERE, "golden", "traj_long.npz"))
     ur = gold["par_coop9_u"]
-    six = lambda vals: ["0" if abs(float(v)) < 1e-12 else "%.6g" % float(v) for v in vals]
     assert len(recs) == 1200
+    ties = 0
     for k, rec in enumerate(recs):
-        assert six(rec["u"].split()) == six(ur[k]), (k, rec["u"], ur[k])
+        eq, tie = GC.six_digit_strings_ok(rec["u"].split(), ur[k])
+        assert eq or tie, (k, rec["u"], ur[k])
+        ties += tie
+    assert ties <= 2, ties
 
 
 LOOP = os.path.join(HERE, "cpp", "distributed_controller_loop")
