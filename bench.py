@@ -318,7 +318,8 @@ def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2,
         for k in range(steps):
             bind(i + k)
             ctx.step(K, cmpc.CMPC_APPLY_MOVE)
-        if markers:
+        if markers:  # (the marker runs on torch's stream: after the pass's kernels)
+            ctx.synchronize()
             torch.cuda._sleep(1000)
         kt = {}
         for kn, kid in (("build", cmpc.CMPC_KERNEL_BUILD), ("iterate", cmpc.CMPC_KERNEL_ITERATE),
