@@ -25,6 +25,7 @@
 // G = Su' W Su_other and f.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "cmpc_internal.h"
 #include "dpp_blocks.inc"
@@ -112,6 +113,30 @@
   }
 #endif
 
+// the role split's chain (build_wave_body SPLIT): CMPC_SPLIT_ILP partial
+// accumulators per chain (its wave has no gather FMAs to interleave; 1 = the
+// single chain of SPLIT = false)
+#ifndef CMPC_SPLIT_ILP
+#define CMPC_SPLIT_ILP 1
+#endif
+#if CMPC_SPLIT_ILP == 2
+#define CMPC_SPLIT_CHAIN(pv, m, a)                  \
+  {                                                 \
+    double a1_ = 0.0;                               \
+    prop2w_dpp<NS, ND>(pv, m, a, a1_);              \
+    a = a + a1_;                                    \
+  }
+#elif CMPC_SPLIT_ILP == 3
+#define CMPC_SPLIT_CHAIN(pv, m, a)                  \
+  {                                                 \
+    double ax_[3] = {a, 0.0, 0.0};                  \
+    prop3w_dpp<NS, ND>(pv, m, ax_);                 \
+    a = (ax_[0] + ax_[1]) + ax_[2];                 \
+  }
+#else
+#define CMPC_SPLIT_CHAIN(pv, m, a) CMPC_EXP_PROP(pv, m, a)
+#endif
+
 // Diagnostic build (tools/rows_timing.py ... wave): per-wave s_memtime cycle
 // totals of the QP phases of the one-QP-per-wave kernel, written over the QP
 // output as the row kernel's CMPC_ROWS_TIMING (results invalid).
@@ -140,7 +165,17 @@
 // (lane_solve.h; a scenario's sub-controllers are adjacent waves, so adjacent
 // lanes).  Even FUSE values record the working-set trace.  The QP is stored
 // either way (cmpc_download_qp).
-template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE>
+//
+// SPLIT (role split, small batches, ny <= 3, FUSE 0-2): two waves per QP in a
+// two-wave workgroup.  Wave 0 stages the record and runs the prologue and the
+// DPP chain of every step (P rows and the free response), storing the raw
+// Markov values into the delay lines and z into a two-block ring; wave 1 runs
+// the gather FMAs one block behind, reading those values, then the epilogue
+// (and the fused solve).  One workgroup barrier per block of up to U steps.
+// The same FMAs in the same order per lane: bit-identical to SPLIT = false,
+// with the two waves' instructions sharing a SIMD's issue slots (one wave per
+// SIMD issues an FP64 VALU about every 8 cycles).
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE, bool SPLIT = false>
 __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -155,12 +190,17 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   // pre-pass (every row simulating, row 3 storing z_r into per-output lines)
   // and the main pass has four P rows whose z lanes read those lines
   constexpr bool PRE = NY == 4;
+  static_assert(!SPLIT || (!PRE && FUSE <= 2), "role split: ny <= 3, row solver");
+  constexpr int WGW = SPLIT ? 2 : CMPC_BUILD_WAVES;  // waves per workgroup
+  constexpr int QPG = SPLIT ? 1 : CMPC_BUILD_WAVES;  // QPs per workgroup at a time
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = SPLIT ? 0 : (threadIdx.x >> 6);   // QP slot of the workgroup
+  const bool wA = !SPLIT || (threadIdx.x >> 6) == 0;   // chain (and prologue) wave
+  const bool wB = !SPLIT || (threadIdx.x >> 6) == 1;   // gather (and epilogue) wave
   const int row = lane >> 4, col = lane & 15;
   const int pp = P.p, S = P.S;
   const int nobs = P.nobs, rec_len = P.rec_len;
-  const int nwaves = gridDim.x * CMPC_BUILD_WAVES;
+  const int nwaves = gridDim.x * QPG;
   const int nchunk = rec_len / 2;
 
   // Delay lines: one per (row o, input c), length D_c + M - 1 + p; the first
@@ -207,13 +247,13 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   double* lines = recl + o_line;
   double* zl = recl + o_zl;
   double* red = lines;
-  for (int e = threadIdx.x; e < S * P.yl_stride; e += 64 * CMPC_BUILD_WAVES) {
+  for (int e = threadIdx.x; e < S * P.yl_stride; e += 64 * WGW) {
     const int ss = e / P.yl_stride, t = e - ss * P.yl_stride;
     yl_all[e] = (t < pp * NY) ? P.cfg[(size_t)ss * P.co.len + P.co.yhat + t] : 0.0;
   }
-  for (int e = threadIdx.x; e < S * NY * NY; e += 64 * CMPC_BUILD_WAVES)
+  for (int e = threadIdx.x; e < S * NY * NY; e += 64 * WGW)
     lw_all[e] = P.cfg[(size_t)(e / (NY * NY)) * P.co.len + P.co.lwt + e % (NY * NY)];
-  for (int e = threadIdx.x; e < S * NU * NU; e += 64 * CMPC_BUILD_WAVES)
+  for (int e = threadIdx.x; e < S * NU * NU; e += 64 * WGW)
     uw_all[e] = P.cfg[(size_t)(e / (NU * NU)) * P.co.len + P.co.uwt + e % (NU * NU)];
   if (threadIdx.x < 16) zeros[threadIdx.x] = 0.0;
   __syncthreads();
@@ -287,12 +327,12 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   double* red_w = red + ((row >= 1 ? row - 1 : 0) * NG + col) * NV;
 
   // ---- prefetch the first record (coalesced 16-byte loads) ----
-  int q = blockIdx.x * CMPC_BUILD_WAVES + wave;
+  int q = blockIdx.x * QPG + wave;
   double2 chunk[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int ci = lane + 64 * i;
-    chunk[i] = (q < P.nqp && ci < nchunk)
+    chunk[i] = (wA && q < P.nqp && ci < nchunk)
                    ? reinterpret_cast<const double2*>(P.lin + (size_t)q * rec_len)[ci]
                    : make_double2(0.0, 0.0);
   }
@@ -308,7 +348,12 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
   const uint64_t t0c = tlast, t0r = __builtin_amdgcn_s_memrealtime();
 #endif
+  bool first_qp = true;
   for (; q < P.nqp; q += nwaves) {
+    if constexpr (SPLIT) {  // the previous QP's epilogue has read its LDS
+      if (!first_qp) __syncthreads();
+      first_qp = false;
+    }
     CMPC_WT(5)  // back-edge
     {
       const int level = 3 - (4 * done_qp) / share;
@@ -324,15 +369,15 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int ci = lane + 64 * i;
-      if (ci < nchunk) reinterpret_cast<double2*>(recl)[ci] = chunk[i];
+      if (wA && ci < nchunk) reinterpret_cast<double2*>(recl)[ci] = chunk[i];
     }
-    if (lane < NUT) uol[lane] = uold_l;
+    if (wA && lane < NUT) uol[lane] = uold_l;
     {
       const int qn = q + nwaves;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int ci = lane + 64 * i;
-        chunk[i] = (qn < P.nqp && ci < nchunk)
+        chunk[i] = (wA && qn < P.nqp && ci < nchunk)
                        ? reinterpret_cast<const double2*>(P.lin + (size_t)qn * rec_len)[ci]
                        : make_double2(0.0, 0.0);
       }
@@ -342,7 +387,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     const double* Cs = recl + P.off_C;
     const double* xa = recl + P.off_x;
     // C_hat = L_W' C_sel (ny x nobs), one element per lane
-    if (prow && col < nobs) {
+    if (wA && prow && col < nobs) {
       double t = 0.0;
 #pragma unroll
       for (int o2 = 0; o2 < NY; ++o2)
@@ -351,7 +396,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     }
     // delay-line inputs w_t (stride NY), AdjustAllDelayedStates applied
     // (include/aug_lin_sys.h:141-154); zero once the delay line has drained
-    for (int e = lane; e < (pp + 3) * NY; e += 64) {
+    for (int e = lane; wA && e < (pp + 3) * NY; e += 64) {
       const int t = e / NY, k = e - t * NY;
       double v = 0.0;
       int dl = 0, bo = 0, di = 0;
@@ -365,7 +410,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
       wl[e] = v;
     }
     // kappa = L_W'(dist + y_prev) = C_hat_dist xa_dist + L_W' y_prev
-    if (prow && col == 15) {
+    if (wA && prow && col == 15) {
       const double* yp = recl + P.off_y;
       double t = 0.0;
       for (int d = 0; d < P.ndist; ++d) t += chat[row * nobs + NS + d] * xa[d];
@@ -442,7 +487,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     // zero the first m-1 entries of every delay line (history before t = 0);
     // the record area the lines overlay is dead once the operands above are
     // in registers
-    if (zero_lane) lines[zero_at] = 0.0;
+    if (wA && zero_lane) lines[zero_at] = 0.0;
     double acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
@@ -474,6 +519,77 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   }
 
     CMPC_WT(2)  // prologue compute
+    if constexpr (SPLIT) {
+      // wave 0: block b of the chain; wave 1: block b - 1 of the gather; one
+      // barrier per block.  z goes through a ring of two blocks (the delay
+      // lines hold the whole horizon).
+      double* zring = recl + P.lds_per_wave;  // NY x 2U
+      const bool zg = glane && col == M * NUT;
+      int rinc_q = rinc, rB = 0, plen = 0, blk = 0;
+#define CMPC_SPLIT_A(u)                                         \
+  {                                                             \
+    double a = an;                                              \
+    CMPC_SPLIT_CHAIN(pv, m, a);                                 \
+    an = __builtin_fma(-ym, yh, base);                          \
+    yh = ylp[((u) + 1) * NY];                                   \
+    pv = a;                                                     \
+    if (mlane || slane) wa[u] = a;                              \
+  }
+#define CMPC_SPLIT_B(u)                                         \
+  {                                                             \
+    const double rd_ = rb[u];                                   \
+    va = __builtin_fma(smask, va, rd_);                         \
+    CMPC_EXP_GACC(va, acc);                                     \
+  }
+#define CMPC_SPLIT_BLOCK(L)                                                        \
+  {                                                                                \
+    if (wA) {                                                                      \
+      if ((L) > 0) {                                                               \
+        double* wa = slane ? zring + oz * (2 * U) + (blk & 1) * U : wq;           \
+        CMPC_SPLIT_A(0)                                                            \
+        if ((L) == U) {                                                            \
+          CMPC_SPLIT_A(1)                                                          \
+          CMPC_SPLIT_A(2)                                                          \
+          CMPC_SPLIT_A(3)                                                          \
+        }                                                                          \
+        wq += (L) * winc;                                                          \
+        ylp += (L) * NY;                                                           \
+      }                                                                            \
+    } else if (plen > 0) {                                                         \
+      const double* rb = zg ? zring + row * (2 * U) + ((blk - 1) & 1) * U : rq;   \
+      CMPC_SPLIT_B(0)                                                              \
+      if (plen == U) {                                                             \
+        CMPC_SPLIT_B(1)                                                            \
+        CMPC_SPLIT_B(2)                                                            \
+        CMPC_SPLIT_B(3)                                                            \
+      }                                                                            \
+      rq += plen * rinc_q;                                                         \
+      rB += plen;                                                                  \
+      if (gdel == rB) { /* delayed input's history is over: its line */            \
+        rq = rline;                                                                \
+        rinc_q = 1;                                                                \
+      }                                                                            \
+    }                                                                              \
+    __syncthreads();                                                               \
+    plen = (L);                                                                    \
+    ++blk;                                                                         \
+  }
+      static_assert(U == 4, "the split block macros unroll four steps");
+      int r = 0;
+      for (int seg = 0; seg <= nbound; ++seg) {
+        int r_end = pp;
+#pragma unroll
+        for (int c = 0; c < NUT; ++c)
+          if (c == seg && seg < nbound) r_end = bnd[c];
+        for (; r + U <= r_end; r += U) CMPC_SPLIT_BLOCK(U)
+        for (; r < r_end; ++r) CMPC_SPLIT_BLOCK(1)
+      }
+      CMPC_SPLIT_BLOCK(0)  // the gather's last block
+#undef CMPC_SPLIT_BLOCK
+#undef CMPC_SPLIT_B
+#undef CMPC_SPLIT_A
+      if (!wB) continue;  // the chain wave waits at the next QP's barrier
+    } else {
     int r = 0;
     int rinc_q = rinc;
     for (int seg = 0; seg <= nbound; ++seg) {
@@ -505,6 +621,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     va = __builtin_fma(smask, va, rd);
     gacc_dpp<NUT, NU, M>(va, acc);  // row p-1
     // (the accumulation at r = 0 adds products of the zero initial va)
+    }
     CMPC_WT(3)  // horizon loop
 
     // reduce over the ny rows through LDS; row 0 of the gather lanes stores
@@ -646,6 +763,27 @@ __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES)
 __attribute__((amdgpu_waves_per_eu(FUSE ? 1 : 4, FUSE ? 1 : 4)))
 void cmpc_build_kernel(BuildParams P) {
   build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(P);
+}
+
+// the role split (build_wave_body SPLIT): a two-wave workgroup per QP, two
+// waves per SIMD
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE = 0>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void cmpc_build_split_kernel(BuildParams P) {
+  build_wave_body<NS, NY, NUT, NU, M, ND, FUSE, true>(P);
+}
+
+// the role split for batches of at most one QP per SIMD (CMPC_BUILD_SPLIT=0
+// in the environment turns it off, for A/B timing)
+static bool build_split_on(const BuildParams& P, int ny) {
+  static const int env = [] {
+    const char* e = getenv("CMPC_BUILD_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  return env != 0 && ny < 4 && P.nqp <= 4 * P.cus;
+}
+static size_t split_lds_bytes(const BuildParams& P, int ny) {
+  return sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave + (size_t)((ny * 8 + 31) / 32 * 32));
 }
 
 // ---------------------------------------------------------------------------
@@ -832,6 +970,15 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
 // ---------------------------------------------------------------------------
 #define BUILD_CASE(NS_, NY_, NU_, M_)                                                  \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {                   \
+    if constexpr (NY_ < 4) {                                                           \
+      if (build_split_on(P, NY_)) {                                                    \
+        const size_t lds2 = split_lds_bytes(P, NY_);                                   \
+        auto k2_ = cmpc_build_split_kernel<NS_, NY_, 4, NU_, M_, 2>;                   \
+        if (lds2 > 64 * 1024) cmpc_allow_lds(reinterpret_cast<const void*>(k2_), lds2); \
+        cmpc_launch(k2_, dim3(P.nqp), dim3(128), lds2, s, P);                          \
+        return 0;                                                                      \
+      }                                                                                \
+    }                                                                                  \
     const size_t lds = sizeof(double) * ((size_t)P.lds_block +                         \
                                          (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);  \
     if (lds > 64 * 1024)                                                               \
