@@ -16,7 +16,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_WAVE, CMPC_SOLVE_AUTO, CMPC_SOLVE_LANE,
+from ._abi import (CMPC_BUILD_AUTO, CMPC_BUILD_ROWS, CMPC_BUILD_SPLIT, CMPC_BUILD_WAVE, CMPC_SOLVE_AUTO, CMPC_SOLVE_LANE,
                    CMPC_SOLVE_ROWS, CMPC_STEP_AUTO, CMPC_STEP_FUSED, CMPC_STEP_SPLIT, CMPC_KERNEL_STEP,
                    CMPC_APPLY_MOVE, CMPC_KERNEL_BUILD, CMPC_KERNEL_ITERATE,
                    CMPC_KERNEL_PRODUCE, CMPC_KERNEL_OBSERVE_POST, CMPC_KERNEL_OBSERVE_PRIOR, CMPC_QP_INFEASIBLE,
@@ -301,11 +301,13 @@ class Context:
 
     def set_build_variant(self, variant: int):
         """CMPC_BUILD_AUTO / CMPC_BUILD_WAVE (one QP per wave) / CMPC_BUILD_ROWS
-        (four QPs per wave, one per DPP row)."""
+        (four QPs per wave, one per DPP row) / CMPC_BUILD_SPLIT (one QP per two
+        waves: chain and gather, ny <= 3)."""
         check(self.lib.cmpc_set_build_variant(self._h, int(variant)), "cmpc_set_build_variant")
 
     def last_build_kernel(self) -> int:
-        """CMPC_BUILD_WAVE / CMPC_BUILD_ROWS: the kernel the last build() ran."""
+        """CMPC_BUILD_WAVE / CMPC_BUILD_ROWS / CMPC_BUILD_SPLIT: the kernel the
+        last build() ran."""
         v = self.lib.cmpc_last_build_kernel(self._h)
         check(min(v, 0), "cmpc_last_build_kernel")
         return v

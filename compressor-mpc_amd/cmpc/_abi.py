@@ -37,6 +37,7 @@ CMPC_KERNEL_COUNT = 6
 CMPC_BUILD_AUTO = 0
 CMPC_BUILD_WAVE = 1
 CMPC_BUILD_ROWS = 2
+CMPC_BUILD_SPLIT = 3
 CMPC_SOLVE_AUTO = 0
 CMPC_SOLVE_LANE = 1
 CMPC_SOLVE_ROWS = 2

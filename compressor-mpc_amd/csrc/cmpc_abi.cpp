@@ -1554,7 +1554,8 @@ static void build_lds_layout(const cmpc_dims& d, const cmpc_layout& L, BuildPara
 
 int cmpc_set_build_variant(cmpc_ctx* c, int variant) {
   if (!c) return fail("null context");
-  if (variant != CMPC_BUILD_AUTO && variant != CMPC_BUILD_WAVE && variant != CMPC_BUILD_ROWS)
+  if (variant != CMPC_BUILD_AUTO && variant != CMPC_BUILD_WAVE && variant != CMPC_BUILD_ROWS &&
+      variant != CMPC_BUILD_SPLIT)
     return fail("cmpc_set_build_variant: unknown variant");
   c->build_variant = variant;
   return 0;
@@ -1583,16 +1584,22 @@ int cmpc_build(cmpc_ctx* c) {
   // batch gives it at least one wave per SIMD; else
   // the one-QP-per-wave kernel, which has four times the waves for a small
   // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
+  // Below one QP per SIMD (ny <= 3) the role-split kernel: two waves per QP
+  // (config 5: 28.1 -> 22.6 us, profiles/r5g_build_split_ab.txt).
   const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
+  const bool split_fit = d.ny < 4 && c->nqp <= 4 * P.cus;
+  if (c->build_variant == CMPC_BUILD_SPLIT && d.ny >= 4)
+    return fail("role-split build kernel needs ny <= 3");
   if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_fill))
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)
     return fail("row-layout build kernel not available for these dimensions");
   c->last_build = CMPC_BUILD_ROWS;
   if (rc) {
+    P.split = c->build_variant == CMPC_BUILD_SPLIT || (c->build_variant == CMPC_BUILD_AUTO && split_fit);
     if (cmpc_launch_build(P, d.ns, d.ny, d.nu, d.m, c->stream))
       return fail("build kernel not instantiated for these dimensions (ns, ny, nu, m)");
-    c->last_build = CMPC_BUILD_WAVE;
+    c->last_build = P.split ? CMPC_BUILD_SPLIT : CMPC_BUILD_WAVE;
   }
   if (check_launch("build kernel")) return -1;
   return tl.end();

@@ -163,6 +163,7 @@ struct BuildParams {
   int nbound;                    // distinct delays 0 < D < p, ascending (loop segments)
   int bound[CMPC_MAX_INPUTS];
   int grid;                      // workgroups needed (one QP per wave); launcher caps it
+  int split;                     // cmpc_launch_build: the role-split kernel (ny <= 3)
   int cus;                       // compute units of the device
   RowsLayout rows;               // row-layout kernel (four QPs per wave)
   // fused step (cmpc_step on small batches): the K Jacobi iterations run in

@@ -773,15 +773,6 @@ void cmpc_build_split_kernel(BuildParams P) {
   build_wave_body<NS, NY, NUT, NU, M, ND, FUSE, true>(P);
 }
 
-// the role split for batches of at most one QP per SIMD (CMPC_BUILD_SPLIT=0
-// in the environment turns it off, for A/B timing)
-static bool build_split_on(const BuildParams& P, int ny) {
-  static const int env = [] {
-    const char* e = getenv("CMPC_BUILD_SPLIT");
-    return e ? atoi(e) : 1;
-  }();
-  return env != 0 && ny < 4 && P.nqp <= 4 * P.cus;
-}
 static size_t split_lds_bytes(const BuildParams& P, int ny) {
   return sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave + (size_t)((ny * 8 + 31) / 32 * 32));
 }
@@ -971,7 +962,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
 #define BUILD_CASE(NS_, NY_, NU_, M_)                                                  \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {                   \
     if constexpr (NY_ < 4) {                                                           \
-      if (build_split_on(P, NY_)) {                                                    \
+      if (P.split) {                                                                   \
         const size_t lds2 = split_lds_bytes(P, NY_);                                   \
         auto k2_ = cmpc_build_split_kernel<NS_, NY_, 4, NU_, M_, 2>;                   \
         if (lds2 > 64 * 1024) cmpc_allow_lds(reinterpret_cast<const void*>(k2_), lds2); \

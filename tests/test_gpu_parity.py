@@ -623,21 +623,55 @@ def test_gpu_survey_config(plant, ctype, p, B, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ctype,p,B,expect", [("coop", 50, 4096, "rows"), ("coop", 100, 4096, "rows"),
-                                              ("cent", 200, 8192, "rows"), ("coop", 50, 64, "wave"),
-                                              ("cent", 200, 1024, "wave")])
-def test_gpu_build_auto_selects_kernel(ctype, p, B, expect):
+@pytest.mark.parametrize("plant,ctype,p,B,expect", [("par", "coop", 50, 4096, "rows"),
+                                                    ("par", "coop", 100, 4096, "rows"),
+                                                    ("par", "cent", 200, 8192, "rows"),
+                                                    ("par", "coop", 50, 64, "split"),
+                                                    ("par", "cent", 200, 1024, "split"),
+                                                    ("ser", "cent", 100, 64, "wave")])
+def test_gpu_build_auto_selects_kernel(plant, ctype, p, B, expect):
     """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel wherever its LDS fits
-    and the batch gives it a wave per SIMD, and the one-QP-per-wave kernel for
-    small batches (SURVEY config 5: cent p = 200, 1 024 QPs); DESIGN.md §3.0."""
-    _, setup, _, _ = setup_for("par", ctype)
-    cfg = cmpc.reference_config("par", ctype, p=p)
+    and the batch gives it a wave per SIMD; below that the role-split kernel
+    up to one QP per SIMD (SURVEY config 5: cent p = 200, 1 024 QPs), the
+    one-QP-per-wave kernel for ny = 4; DESIGN.md §3.0."""
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
     lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=5, n_distinct=min(B, 256))
     with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
         ctx.build()
         got = ctx.last_build_kernel()
-    assert got == {"rows": cmpc.CMPC_BUILD_ROWS, "wave": cmpc.CMPC_BUILD_WAVE}[expect]
+    assert got == {"rows": cmpc.CMPC_BUILD_ROWS, "wave": cmpc.CMPC_BUILD_WAVE, "split": cmpc.CMPC_BUILD_SPLIT}[expect]
+
+
+SPLIT_CASES = [("par", "cent", 200, None), ("par", "coop", 50, None), ("par", "ncoop", 20, None),
+               ("ser", "ncoop", 80, None), ("par", "coop", 50, (0, 10, 0, 25)), ("par", "cent", 60, (0, 45, 0, 45))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plant,ctype,p,delays", SPLIT_CASES)
+def test_gpu_build_split_equals_wave_bitwise(plant, ctype, p, delays):
+    """The role-split build (chain wave + gather wave, one barrier per block,
+    z through a two-block ring) gives the one-QP-per-wave kernel's H, f and G
+    bit for bit: the same FMAs in the same order per lane."""
+    import dataclasses
+    _, setup, _, _ = setup_for(plant, ctype)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    if delays is not None:
+        cfg = dataclasses.replace(cfg, delays=tuple(delays))
+    arr = cmpc.controller_arrays(cfg, setup)
+    B = 97
+    lin, u_old, du_old, ws = synthetic_batch(cfg, B, seed=41 + p, n_distinct=B)
+    out = {}
+    with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        for v in (cmpc.CMPC_BUILD_WAVE, cmpc.CMPC_BUILD_SPLIT):
+            ctx.set_build_variant(v)
+            ctx.build()
+            assert ctx.last_build_kernel() == v
+            out[v] = ctx.download_qp()
+    for a, b in zip(out[cmpc.CMPC_BUILD_WAVE], out[cmpc.CMPC_BUILD_SPLIT]):
+        assert np.array_equal(a, b)
+        assert np.isfinite(a).all()
 
 
 def test_gpu_bound_state_rotation():
