@@ -337,7 +337,7 @@ def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2,
         bkern = "cmpc_build_rows_kernel" if ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS else "cmpc_build_kernel"
         L = ctx.layout
         restore()
-        changes, _ = traced_changes(ctx, K, bind, range(i, i + NB))
+        changes, _ = traced_changes(ctx, K, bind, range(i, i + steps))  # the timed steps, replayed
         for st_, sn in zip(sts, snap):
             for a, a0 in zip(st_, sn):
                 a.copy_(a0)
