@@ -80,7 +80,13 @@ inline void cmpc_allow_lds(const void* kernel, size_t bytes) {
 #endif
 #define CMPC_ROWS_NSEG 16        // loop segment bounds of the row build kernel
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
-#define CMPC_SOLVE_THREADS 256   // QPs (= lanes) per solve workgroup
+// QPs (= lanes) per solve workgroup: one wave, so a batch of fewer waves than
+// CUs spreads one wave per CU (the CU's scalar unit and instruction fetch
+// are shared by its waves): config 2 iterate (K = 9, 128 waves) 11.6 -> 9.8 us
+// against 256; level at the bench size (profiles/r5h_solve_wg_ab.txt)
+#ifndef CMPC_SOLVE_THREADS
+#define CMPC_SOLVE_THREADS 64
+#endif
 #define CMPC_HOST_OUT_MAX_QP 64  // up to this many QPs: du/status/nWSR live in page-locked host memory
 #ifndef CMPC_SOLVE_ROWS_MAX_QP
 #define CMPC_SOLVE_ROWS_MAX_QP 16384  // CMPC_SOLVE_AUTO: the row solve kernel below this many QPs

@@ -89,12 +89,17 @@ ctx.close()
 ctx = cmpc.Context(cfg, B)
 ctx.configure(arr)
 restore()
-tot = []
+tot, per_it, waves_it = [], np.zeros(9, np.int64), np.zeros(9, np.int64)
 for i in range(40):
     bind(i)
     ctx.step(9, cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE)
     _, ntr = ctx.download_trace(9)
     tot.append((int(ntr.sum()), int((ntr.sum(axis=1) > 0).sum()),
                 int((ntr.reshape(-1, 32, 9).sum(axis=(1, 2)) > 0).sum())))
+    if i >= 8:  # past the restored snapshot's first visit of each batch
+        per_it += ntr.sum(axis=0)
+        waves_it += (ntr.reshape(-1, 64, 9).sum(axis=1) > 0).sum(axis=0)
 print("changes per step (total, QPs with a change, 32-QP groups with a change):", tot, flush=True)
+print("steps 8-39, per Jacobi iteration: changes", per_it.tolist(), "waves with a change", waves_it.tolist(),
+      "(of", 32 * ntr.shape[0] // 64, "wave-steps)", flush=True)
 ctx.close()
