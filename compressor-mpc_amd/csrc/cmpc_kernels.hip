@@ -348,8 +348,10 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
   const uint64_t t0c = tlast, t0r = __builtin_amdgcn_s_memrealtime();
 #endif
+  // (SPLIT: one QP per workgroup, the launcher's grid covers the batch: no
+  // loop-carried state, so the fused solve has the registers of the build)
   bool first_qp = true;
-  for (; q < P.nqp; q += nwaves) {
+  for (; q < P.nqp; q = SPLIT ? P.nqp : q + nwaves) {
     if constexpr (SPLIT) {  // the previous QP's epilogue has read its LDS
       if (!first_qp) __syncthreads();
       first_qp = false;
@@ -373,7 +375,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     }
     if (wA && lane < NUT) uol[lane] = uold_l;
     {
-      const int qn = q + nwaves;
+      const int qn = SPLIT ? P.nqp : q + nwaves;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int ci = lane + 64 * i;
@@ -773,6 +775,9 @@ void cmpc_build_split_kernel(BuildParams P) {
   build_wave_body<NS, NY, NUT, NU, M, ND, FUSE, true>(P);
 }
 
+#ifndef CMPC_STEP_SPLIT_BUILD
+#define CMPC_STEP_SPLIT_BUILD 0  // 1: fused centralized steps on the role-split kernel (config 5 36.5 vs 32.6 us: the row solver spills 92 VGPRs at the split's 256; profiles/r5g_build_split_ab.txt)
+#endif
 static size_t split_lds_bytes(const BuildParams& P, int ny) {
   return sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave + (size_t)((ny * 8 + 31) / 32 * 32));
 }
@@ -991,6 +996,16 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
       return -1;                                                                         \
     const size_t lds = sizeof(double) * ((size_t)P.lds_block +                           \
                                          (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);    \
+    if constexpr (NY_ < 4 && CMPC_STEP_SPLIT_BUILD) {                                    \
+      if (P.nqp <= 4 * P.cus) {                                                          \
+        const size_t lds2 = split_lds_bytes(P, NY_);                                     \
+        auto k2_ = P.sv.trace ? cmpc_build_split_kernel<NS_, NY_, 4, NU_, M_, 2, 2>      \
+                              : cmpc_build_split_kernel<NS_, NY_, 4, NU_, M_, 2, 1>;     \
+        if (lds2 > 64 * 1024) cmpc_allow_lds(reinterpret_cast<const void*>(k2_), lds2);  \
+        cmpc_launch(k2_, dim3(P.nqp), dim3(128), lds2, s, P);                            \
+        return 0;                                                                        \
+      }                                                                                  \
+    }                                                                                    \
     if (P.sv.trace) {                                                                    \
       auto k_ = cmpc_build_kernel<NS_, NY_, 4, NU_, M_, 2, 2>;                           \
       if (lds > 64 * 1024)                                                               \
