@@ -688,8 +688,14 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // the totals are read before the scratch is written
       CMPC_WT(4)  // epilogue
-      rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
-                                                red + NY * NG * NV + row * N * N);
+      if constexpr (SPLIT) {  // the factor in LDS (registers: two waves per SIMD)
+        double* lsh = recl + P.lds_per_wave + (NY * 8 + 31) / 32 * 32 + row * N * N;
+        rows_solve_qp<N, NU, 0, FUSE == 2, false, true>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
+                                                        red + NY * NG * NV + row * N * N, lsh);
+      } else {
+        rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
+                                                  red + NY * NG * NV + row * N * N);
+      }
       __builtin_amdgcn_wave_barrier();
       CMPC_WT(1)  // fused solve
       continue;
@@ -776,10 +782,16 @@ void cmpc_build_split_kernel(BuildParams P) {
 }
 
 #ifndef CMPC_STEP_SPLIT_BUILD
-#define CMPC_STEP_SPLIT_BUILD 0  // 1: fused centralized steps on the role-split kernel (config 5 36.5 vs 32.6 us: the row solver spills 92 VGPRs at the split's 256; profiles/r5g_build_split_ab.txt)
+// 1: fused centralized steps on the role-split kernel, the row solver's
+// factor in LDS to fit 256 VGPRs (5 VGPRs of spills left).  Measured slower
+// at config 5 (35.0 vs 32.5 us per step, 43.2 vs 37.2 us with the move: the
+// solve runs on one wave of the pair with its factor behind LDS latency),
+// profiles/r5g_build_split_ab.txt
+#define CMPC_STEP_SPLIT_BUILD 0
 #endif
 static size_t split_lds_bytes(const BuildParams& P, int ny) {
-  return sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave + (size_t)((ny * 8 + 31) / 32 * 32));
+  // + the z ring (ny x 2U) + four N x N factor areas of the fused row solver
+  return sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave + (size_t)((ny * 8 + 31) / 32 * 32) + 256);
 }
 
 // ---------------------------------------------------------------------------

@@ -151,18 +151,21 @@ CMPC_HD double ndot(const double (&n)[N], const double (&v)[N]) {
 #ifndef CMPC_WSET_STORE_MAX
 #define CMPC_WSET_STORE_MAX 0  // largest N whose working sets store their normals and bounds
 #endif
-template <int N, bool SN = (N <= CMPC_WSET_STORE_MAX)>
+// LS: storage of the factor L, indexed L[i][k]: registers (a plain array), or
+// an LDS matrix (qp_solver_row.h LdsMat, the fused row solver's registers)
+template <int N, bool SN = (N <= CMPC_WSET_STORE_MAX), class LS = double[N][N]>
 struct WSet {
   int K;
   int j[N], side[N];
   double lam[N];
   double nrm[SN ? N : 1][N], bta[SN ? N : 1];  // normals and bounds (SN) or rebuilt from (j, side)
-  double L[N][N], D[N], R[N];
+  LS L;
+  double D[N], R[N];
 };
 
 // the normal of slot a (stored, or rebuilt from its constraint index)
-template <int N, bool SN, class Q>
-CMPC_HD void wset_normal(const Q& q, const WSet<N, SN>& W, int a, double (&n)[N]) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD void wset_normal(const Q& q, const WSet<N, SN, LS>& W, int a, double (&n)[N]) {
   if constexpr (SN) {
 #pragma unroll
     for (int c = 0; c < N; ++c) n[c] = W.nrm[a][c];
@@ -172,16 +175,16 @@ CMPC_HD void wset_normal(const Q& q, const WSet<N, SN>& W, int a, double (&n)[N]
 }
 
 // the bound beta of slot a (stored, or from its constraint index)
-template <int N, bool SN, class Q>
-CMPC_HD double wset_beta(const Q& q, const WSet<N, SN>& W, int a) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD double wset_beta(const Q& q, const WSet<N, SN, LS>& W, int a) {
   if constexpr (SN) return W.bta[a];
   else return q.beta(W.j[a], W.side[a]);
 }
 
 // H^-1 n_a of slot a: columns of an LDS-resident H^-1 (runtime addresses),
 // else the explicit normal's product (registers take compile-time indices)
-template <int N, bool SN, class Q>
-CMPC_HD void wset_h(const Q& q, const WSet<N, SN>& W, int a, double (&out)[N]) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD void wset_h(const Q& q, const WSet<N, SN, LS>& W, int a, double (&out)[N]) {
   if constexpr (Q::HS_t::kColumns) {
     q.hcol(W.j[a], W.side[a], out);
   } else {
@@ -192,8 +195,8 @@ CMPC_HD void wset_h(const Q& q, const WSet<N, SN>& W, int a, double (&out)[N]) {
 }
 // n_a' v of slot a (the explicit normal's FMAs: fewer instructions than
 // selecting v's entries by the runtime constraint index)
-template <int N, bool SN, class Q>
-CMPC_HD double wset_dot(const Q& q, const WSet<N, SN>& W, int a, const double (&v)[N]) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD double wset_dot(const Q& q, const WSet<N, SN, LS>& W, int a, const double (&v)[N]) {
   double n[N];
   wset_normal(q, W, a, n);
   return ndot<N>(n, v);
@@ -214,8 +217,8 @@ CMPC_HD void q_h(const Q& q, int j, int side, double (&out)[N]) {
 // pivots R = 1/D (or_qp.c ldl); returns false unless every pivot
 // d_j > rel * M_jj (rel = 0: H positive definite; TOL_Z: a working set with
 // independent normals).
-template <int N>
-CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D)[N],
+template <int N, class LM>
+CMPC_HD bool ldl_k(int K, const double (&M)[N][N], LM& L, double (&D)[N],
                    double (&R)[N], double rel = 0.0) {
   bool ok = true;
 #pragma unroll
@@ -248,8 +251,8 @@ CMPC_HD bool ldl_k(int K, const double (&M)[N][N], double (&L)[N][N], double (&D
 // forward step is one block under `i < K`, so a wave skips the steps past the
 // largest working set among its lanes; every computed entry has the
 // arithmetic of the plain loops, bit for bit.
-template <int N>
-CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
+template <int N, class LM>
+CMPC_HD void ldl_solve_k(int K, const LM& L, const double (&R)[N],
                          const double (&b)[N], double (&x)[N], double (&zz)[N]) {
   double y[N];
 #pragma unroll
@@ -277,8 +280,8 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
     }
   }
 }
-template <int N>
-CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
+template <int N, class LM>
+CMPC_HD void ldl_solve_k(int K, const LM& L, const double (&R)[N],
                          const double (&b)[N], double (&x)[N]) {
   double zz[N];
   ldl_solve_k<N>(K, L, R, b, x, zz);
@@ -286,8 +289,8 @@ CMPC_HD void ldl_solve_k(int K, const double (&L)[N][N], const double (&R)[N],
 
 // warm start: M (M[i][k] = n_k' Hinv n_i, k <= i) of the current slots and
 // its LDL' (or_qp.c wset_factor)
-template <int N, bool SN, class Q>
-CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD bool wset_factor(const Q& q, WSet<N, SN, LS>& W) {
   double M[N][N];
 #pragma unroll
   for (int b = 0; b < N; ++b) {
@@ -310,8 +313,8 @@ CMPC_HD bool wset_factor(const Q& q, WSet<N, SN>& W) {
 // remove slot a (or_qp.c wset_remove): the other slots keep their order; the
 // trailing block of the factor takes the rank-one term D_a w w' (GGMS method
 // C1, reciprocal pivots), then rows and columns after a move up by one
-template <int N, bool SN>
-CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
+template <int N, bool SN, class LS>
+CMPC_HD void wset_drop(WSet<N, SN, LS>& W, int a) {
   double w[N];
   double alpha = 0.0;
 #pragma unroll
@@ -366,8 +369,8 @@ CMPC_HD void wset_drop(WSet<N, SN>& W, int a) {
 
 // append (j, side) as slot K (or_qp.c wset_append): the bordered factor's
 // row zz = D^-1 L^-1 qv and pivot zn (= den - qv' M^-1 qv), R = 1/zn
-template <int N, bool SN>
-CMPC_HD void wset_add(WSet<N, SN>& W, int j, int side, double lam, const double (&n)[N], double bta,
+template <int N, bool SN, class LS>
+CMPC_HD void wset_add(WSet<N, SN, LS>& W, int j, int side, double lam, const double (&n)[N], double bta,
                       const double (&zz)[N], double zn, double rzn) {
 #pragma unroll
   for (int b = 0; b < N; ++b)
@@ -433,8 +436,8 @@ CMPC_HD bool hinv_of(const double (&H)[N][N], HS& Hinv) {
 constexpr uint32_t kWsInvalid = 0xFFFFFFFFu;
 
 // the warm start's slots: the constraints of ws_in in ascending j
-template <int N, bool SN, class Q>
-CMPC_HD void wset_fill(const Q& q, uint32_t ws_in, WSet<N, SN>& W) {
+template <int N, bool SN, class LS, class Q>
+CMPC_HD void wset_fill(const Q& q, uint32_t ws_in, WSet<N, SN, LS>& W) {
   W.K = 0;
   uint32_t msk = ws_in & ((1u << (2 * N)) - 1u);
 #pragma unroll
@@ -455,8 +458,8 @@ CMPC_HD void wset_fill(const Q& q, uint32_t ws_in, WSet<N, SN>& W) {
   }
 }
 
-template <bool TRACE, int N, int NU, int NB, class HS, bool SN>
-CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[N], int chg, bool done,
+template <bool TRACE, int N, int NU, int NB, class HS, bool SN, class LS>
+CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN, LS>& W, double (&x)[N], int chg, bool done,
                         int max_chg, QpOut& o);
 
 // The plain solve (standalone QPs, InitializeQPProblem, the coupled
@@ -543,8 +546,8 @@ CMPC_HD void qp_solve_t(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const
 
 // Phase B (Goldfarb–Idnani) from the phase-A point x and multipliers W.lam,
 // then the result: working-set word, finite check, bound fixing / zero move.
-template <bool TRACE, int N, int NU, int NB, class HS, bool SN>
-CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN>& W, double (&x)[N], int chg, bool done,
+template <bool TRACE, int N, int NU, int NB, class HS, bool SN, class LS>
+CMPC_HD void qp_phase_b(const Qp<N, NU, NB, HS>& q, WSet<N, SN, LS>& W, double (&x)[N], int chg, bool done,
                         int max_chg, QpOut& o) {
   // B. Goldfarb–Idnani
   for (int outer = 0; outer <= max_chg + 1 && !done && CMPC_QP_ABL != 1; ++outer) {
@@ -751,8 +754,8 @@ struct UStrided {
 // explicit normal is formed once and serves all 1 + NVO right-hand sides
 // (N' x_u0 and N' U's columns: FMAs with 0 / +-1 coefficients, exact, the
 // oracle's nu_dot values).
-template <int N, int NVO, int NU, int NB, class HS, bool SN, class UA>
-CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const double (&xu0)[N],
+template <int N, int NVO, int NU, int NB, class HS, bool SN, class LS, class UA>
+CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN, LS>& W, const double (&xu0)[N],
                         const UA& U, JMap<N, NVO>& mp) {
   constexpr int NVOA = JMap<N, NVO>::NVOA;
   double rhs0[N], rc[NVOA][N];
@@ -804,8 +807,8 @@ CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN>& W, const 
 }
 
 // the working-set word of the first K slots
-template <int N, bool SN>
-CMPC_HD uint32_t wset_word(const WSet<N, SN>& W) {
+template <int N, bool SN, class LS>
+CMPC_HD uint32_t wset_word(const WSet<N, SN, LS>& W) {
   uint32_t w = 0;
 #pragma unroll
   for (int a = 0; a < N; ++a)

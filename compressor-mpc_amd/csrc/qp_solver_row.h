@@ -1,6 +1,6 @@
 // Row-parallel form of the QP solver (qp_solver.h) for batches too small to
 // fill the GPU with one QP per lane: one QP per 16-lane DPP row, four per
-// wave64.  Same specification (oracle/or_qp.c, version 3) and arithmetic
+// wave64.  Same specification (oracle/or_qp.c, version 4) and arithmetic
 // order as qp_solve_t, bit for bit:
 //  - vectors stay distributed: lane l < N holds row l of H^-1 (registers and
 //    this QP's N x N LDS scratch T), and entry l of x_u, x, H^-1 nu_p, z;
@@ -56,6 +56,22 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<N, C + 1>(f);
   }
 }
+
+// The working set's factor L in LDS (one N x N matrix per row, every lane of
+// the row reading and writing the same values): WSet<N, false, LdsMat<N>>
+// frees the 2 N (N - 1) / 2 registers of the replicated factor where the row
+// solver shares a kernel with other register-hungry code (the fused split step).
+template <int N>
+struct LdsMat {
+  double* p;
+  struct Row {
+    double* r;
+    __device__ __forceinline__ double& operator[](int k) const { return r[k]; }
+  };
+  __device__ __forceinline__ Row operator[](int i) const { return Row{p + i * N}; }
+};
+template <int N, bool LDSL>
+using RowWSet = WSet<N, false, std::conditional_t<LDSL, LdsMat<N>, double[N][N]>>;
 
 // No stored H^-1 (the Qp's bounds, thresholds and normals only)
 struct NoHinv {
@@ -155,8 +171,8 @@ __device__ __forceinline__ double nval(double v, int rowbase, int j, int side) {
 // warm start: the LDL' of M (M[i][k] = n_k' h_i, k <= i; wset_factor) with
 // the h_i distributed (hv[i] = entry l of h_i) and M's entries formed where
 // the factorisation reads them, in ldl_k's order
-template <int N, int NU>
-__device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowbase, WSet<N, false>& W) {
+template <int N, int NU, class WS>
+__device__ __forceinline__ bool wset_factor_row(const double* t, int l, int rowbase, WS& W) {
   double hv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) hv[i] = (i < W.K) ? hval<N, NU>(t, l, W.j[i], W.side[i]) : 0.0;
@@ -243,9 +259,9 @@ __device__ __forceinline__ int row_scan(double x_l, const RowScan& sc, uint32_t 
 
 // Phase B (Goldfarb–Idnani) of the row's QP from the phase-A point x_l and
 // multipliers W.lam, then the result (qp_phase_b).
-template <bool TRACE, int N, int NU>
+template <bool TRACE, int N, int NU, class WS>
 __device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const double* t, const RowScan& sc,
-                                               int l, int rowbase, WSet<N, false>& W, double& x_l, int chg,
+                                               int l, int rowbase, WS& W, double& x_l, int chg,
                                                bool done, int max_chg, QpOut& o) {
   // B. Goldfarb–Idnani
   for (int outer = 0; outer <= max_chg + 1 && !done; ++outer) {
@@ -364,12 +380,14 @@ __device__ __forceinline__ void qp_row_phase_b(const RowQp<N, NU>& q, const doub
 // qp_solve_t for the QP of this row: g_l = entry l of
 // the gradient, t = hinv_row's LDS scratch, hr = row l of H^-1, sc the scan
 // constants; x_l = entry l of the solution (zero on failure).
-template <bool TRACE, int N, int NU>
+template <bool TRACE, int N, int NU, bool LDSL = false>
 __device__ __forceinline__ void qp_solve_row(const RowQp<N, NU>& q, const double (&hr)[N], const double* t,
                                              const RowScan& sc, int l, bool pd, double tol_d, double g_l,
-                                             uint32_t ws_in, int max_chg, double& x_l, QpOut& o) {
+                                             uint32_t ws_in, int max_chg, double& x_l, QpOut& o,
+                                             double* lsh = nullptr) {
   const int rowbase = (int)(__lane_id() & ~15u);
-  WSet<N, false> W;
+  RowWSet<N, LDSL> W;
+  if constexpr (LDSL) W.L.p = lsh;
   o.status = CMPC_QP_OK;
   o.nchg = 0;
   o.ntrace = 0;
@@ -491,9 +509,9 @@ __device__ __forceinline__ void row_jmap_terms(const double (&hr)[N], double f_l
   }
 }
 
-template <int N, int NU, int NVO>
+template <int N, int NU, int NVO, class WS>
 __device__ __forceinline__ void row_jmap_build(const RowQp<N, NU>& q, const double* t, int l, int rowbase,
-                                               const WSet<N, false>& W,
+                                               const WS& W,
                                                double xu0_l, const double (&U_l)[RowMap<N, NVO>::NVOA],
                                                RowMap<N, NVO>& mp) {
   double rhs[N];
@@ -525,14 +543,16 @@ __device__ __forceinline__ void row_jmap_build(const RowQp<N, NU>& q, const doub
 
 // qp_solve_map for the row's QP (xu0_l, U_l from row_jmap_terms; d the
 // other plans, replicated); mp persists across the QP's iterations
-template <bool TRACE, int N, int NU, int NVO>
+template <bool TRACE, int N, int NU, int NVO, bool LDSL = false>
 __device__ __forceinline__ void qp_solve_row_map(const RowQp<N, NU>& q, const double* t, const RowScan& sc, int l,
                                                  bool pd, double tol_d, double xu0_l,
                                                  const double (&U_l)[RowMap<N, NVO>::NVOA],
                                                  const double (&d)[RowMap<N, NVO>::NVOA], uint32_t ws_in,
-                                                 int max_chg, double& x_l, QpOut& o, RowMap<N, NVO>& mp) {
+                                                 int max_chg, double& x_l, QpOut& o, RowMap<N, NVO>& mp,
+                                                 double* lsh = nullptr) {
   const int rowbase = (int)(__lane_id() & ~15u);
-  WSet<N, false> W;
+  RowWSet<N, LDSL> W;
+  if constexpr (LDSL) W.L.p = lsh;
   o.status = CMPC_QP_OK;
   o.nchg = 0;
   o.ntrace = 0;

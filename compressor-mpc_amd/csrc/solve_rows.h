@@ -12,10 +12,13 @@
 #include "cmpc_internal.h"
 #include "qp_solver_row.h"
 
-template <int N, int NU, int NVO, bool TRACE, bool EXT>
+// LDSL: the working-set factor in this row's N x N LDS area lsh (registers
+// otherwise; qp_solver_row.h LdsMat)
+template <int N, int NU, int NVO, bool TRACE, bool EXT, bool LDSL = false>
 __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool active, int s, int l,
                                               int base_lane, const double (&Hl)[N], double f_l,
-                                              const double (&Gl)[NVO > 0 ? NVO : 1], double* tsh) {
+                                              const double (&Gl)[NVO > 0 ? NVO : 1], double* tsh,
+                                              double* lsh = nullptr) {
   constexpr int M = N / NU;
   constexpr int NVOA = NVO > 0 ? NVO : 1;
   constexpr int SM1 = NVO / N;  // other sub-controllers per scenario
@@ -59,7 +62,7 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
   double x_l = 0.0;
   QpOut o;
   if (P.init) {  // InitializeQPProblem: cold solve of the step QP, status ignored
-    qp_solve_row<false, N, NU>(qp, hr, tsh, sc, l, pd, tol_d, f_l, 0u, CMPC_NWSR_MAX, x_l, o);
+    qp_solve_row<false, N, NU, LDSL>(qp, hr, tsh, sc, l, pd, tol_d, f_l, 0u, CMPC_NWSR_MAX, x_l, o, lsh);
     if (active && l == 0) P.ws[q] = o.ws;
     __builtin_amdgcn_wave_barrier();  // tsh is reused by the next QP of this row
     return;
@@ -109,8 +112,8 @@ __device__ __forceinline__ void rows_solve_qp(const SolveParams& P, int q, bool 
       }
     }
     // f_k = f + G du_other, in the map form
-    qp_solve_row_map<TRACE, N, NU, NVO>(qp, tsh, sc, l, pd, tol_d, xu0_l, U_l, dother, ws, CMPC_NWSR_MAX, x_l, o,
-                                        mp);
+    qp_solve_row_map<TRACE, N, NU, NVO, LDSL>(qp, tsh, sc, l, pd, tol_d, xu0_l, U_l, dother, ws, CMPC_NWSR_MAX, x_l,
+                                              o, mp, lsh);
     ws = o.ws;
     dprev_l = x_l;
     if (TRACE && active && l == 0 && P.trace) {
