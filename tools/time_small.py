@@ -22,7 +22,8 @@ CONFIGS = {  # name: (plant, controller, p, B scenarios, K)
     "head": ("par", "coop", 50, 65536, 9),
 }
 REPS = int(os.environ.get("CMPC_TS_REPS", "50"))
-VARS = [("wave", cmpc.CMPC_BUILD_WAVE), ("rows", cmpc.CMPC_BUILD_ROWS), ("auto", cmpc.CMPC_BUILD_AUTO)]
+VARS = [("wave", cmpc.CMPC_BUILD_WAVE), ("split", getattr(cmpc, "CMPC_BUILD_SPLIT", -1)),
+        ("rows", cmpc.CMPC_BUILD_ROWS), ("auto", cmpc.CMPC_BUILD_AUTO)]
 
 
 def settle(ctx, K, sec=0.3):
