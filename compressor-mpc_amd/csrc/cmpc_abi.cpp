@@ -1584,12 +1584,10 @@ int cmpc_build(cmpc_ctx* c) {
   // batch gives it at least one wave per SIMD; else
   // the one-QP-per-wave kernel, which has four times the waves for a small
   // batch (cent p = 200, 1 024 QPs: 0.026 vs 0.057 ms)
-  // Below one QP per SIMD (ny <= 3) the role-split kernel: two waves per QP
+  // Below one QP per SIMD the role-split kernel: two waves per QP
   // (config 5: 28.1 -> 22.6 us, profiles/r5g_build_split_ab.txt).
   const bool rows_fill = (c->nqp + 3) / 4 >= 4 * P.cus;
-  const bool split_fit = d.ny < 4 && c->nqp <= 4 * P.cus;
-  if (c->build_variant == CMPC_BUILD_SPLIT && d.ny >= 4)
-    return fail("role-split build kernel needs ny <= 3");
+  const bool split_fit = c->nqp <= 4 * P.cus;
   if (c->build_variant == CMPC_BUILD_ROWS || (c->build_variant == CMPC_BUILD_AUTO && rows_fill))
     rc = cmpc_launch_build_rows(P, d.ns, d.ny, d.nu, d.m, c->stream);
   if (rc && c->build_variant == CMPC_BUILD_ROWS)
@@ -1917,7 +1915,11 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   // solver of wave 0 after a workgroup barrier for S = 2, 4), the row kernel
   // from one row group per SIMD up to 16 384 QPs (config 2)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP;
+  // (up to one QP per CU AUTO runs the role-split build and the iterate
+  // kernel instead: cent-ser B = 1 21.8 vs 24.4 us, coop-par B = 1 19.3 vs
+  // 19.9 us; config 5, 1 024 QPs, stays fused: 37.2 vs 38.4 us with the move,
+  // profiles/r5j_split_step_ab.txt)
+  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && c->nqp > std::max(c->cus, 1);
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
                     (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);

@@ -190,7 +190,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   // pre-pass (every row simulating, row 3 storing z_r into per-output lines)
   // and the main pass has four P rows whose z lanes read those lines
   constexpr bool PRE = NY == 4;
-  static_assert(!SPLIT || (!PRE && FUSE <= 2), "role split: ny <= 3, row solver");
+  static_assert(!SPLIT || FUSE <= 2, "role split: the row solver");
   constexpr int WGW = SPLIT ? 2 : CMPC_BUILD_WAVES;  // waves per workgroup
   constexpr int QPG = SPLIT ? 1 : CMPC_BUILD_WAVES;  // QPs per workgroup at a time
   const int lane = threadIdx.x & 63;
@@ -421,7 +421,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
         if (o2 >= row) t += lwt[row * NY + o2] * yp[o2];
       kap[row] = t;
     }
-    if constexpr (PRE) {
+    if constexpr (PRE) if (wA) {
       // free-response pre-pass: the row-3 lane roles of the ny <= 3 layout in
       // every row (states j < ns, outputs ns + o, delayed-input carriers in
       // the top ND lanes); row 3's output lanes store z_r at zl[o][r]
@@ -526,14 +526,16 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
       // barrier per block.  z goes through a ring of two blocks (the delay
       // lines hold the whole horizon).
       double* zring = recl + P.lds_per_wave;  // NY x 2U
-      const bool zg = glane && col == M * NUT;
+      const bool zg = !PRE && glane && col == M * NUT;  // (PRE: z lines, read as the delay lines)
       int rinc_q = rinc, rB = 0, plen = 0, blk = 0;
 #define CMPC_SPLIT_A(u)                                         \
   {                                                             \
     double a = an;                                              \
     CMPC_SPLIT_CHAIN(pv, m, a);                                 \
-    an = __builtin_fma(-ym, yh, base);                          \
-    yh = ylp[((u) + 1) * NY];                                   \
+    if constexpr (!PRE) {                                       \
+      an = __builtin_fma(-ym, yh, base);                        \
+      yh = ylp[((u) + 1) * NY];                                 \
+    }                                                           \
     pv = a;                                                     \
     if (mlane || slane) wa[u] = a;                              \
   }
@@ -978,7 +980,7 @@ __global__ __launch_bounds__(CMPC_SOLVE_THREADS) void cmpc_qp_batch_kernel(QpBat
 // ---------------------------------------------------------------------------
 #define BUILD_CASE(NS_, NY_, NU_, M_)                                                  \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {                   \
-    if constexpr (NY_ < 4) {                                                           \
+    {                                                                                  \
       if (P.split) {                                                                   \
         const size_t lds2 = split_lds_bytes(P, NY_);                                   \
         auto k2_ = cmpc_build_split_kernel<NS_, NY_, 4, NU_, M_, 2>;                   \

@@ -325,7 +325,7 @@ def compare_step(B, S, K, dev, orc, margin, excused):
     return diff & ~flag & ~excused, diff & (flag | excused)
 
 
-def _step_parity(cfg, setup, K, B=96, seed=100, expect_fused=None, threads=1):
+def _step_parity(cfg, setup, K, B=96, seed=100, expect_fused=None, threads=1, step_variant=None):
     """Three closed-loop steps (state persists: ws, du_old, u_old with the
     first move applied), device and oracle each on their own state: plans
     within tolerance, statuses, nWSR, working sets and the working-set change
@@ -339,6 +339,8 @@ def _step_parity(cfg, setup, K, B=96, seed=100, expect_fused=None, threads=1):
     nq = B * cfg.S
     excused = np.zeros(B, bool)
     with make_ctx(cfg, arr, B, lin, u_old, du_old, ws) as ctx:
+        if step_variant is not None:
+            ctx.set_step_variant(step_variant)
         for step in range(3):
             flags = cmpc.CMPC_APPLY_MOVE | cmpc.CMPC_TRACE
             if step == 0:
@@ -380,14 +382,16 @@ def test_gpu_step_matches_oracle(plant, ctype, p, K):
 @pytest.mark.parametrize("plant,ctype,p,K,B", [("par", "cent", 200, 1, 1024),   # SURVEY config 5
                                               ("par", "coop", 50, 9, 1)])      # the B = 1 call
 def test_gpu_fused_step_matches_oracle(plant, ctype, p, K, B):
-    """_step_parity through the fused one-launch steps CMPC_STEP_AUTO runs at
-    these sizes (config 5: the one-QP-per-wave build with the row solver in
-    the same kernel; B = 1 coop-par: the fused step), each step after the
-    first checked to have run fused, directly against the oracle over three
-    steps with the move applied."""
+    """_step_parity through the fused one-launch steps at these sizes
+    (config 5: the one-QP-per-wave build with the row solver in the same
+    kernel; B = 1 coop-par: the fused step with the lane solver; pinned with
+    CMPC_STEP_FUSED; AUTO runs the split build and the iterate kernel at B = 1),
+    each step after the first checked to have run fused, directly against the
+    oracle over three steps with the move applied; then the same through AUTO."""
     _, setup, _, _ = setup_for(plant, ctype)
-    _step_parity(cmpc.reference_config(plant, ctype, p=p), setup, K, B=B, seed=300 + p, expect_fused=1,
-                 threads=8)
+    cfg = cmpc.reference_config(plant, ctype, p=p)
+    _step_parity(cfg, setup, K, B=B, seed=300 + p, expect_fused=1, threads=8, step_variant=cmpc.CMPC_STEP_FUSED)
+    _step_parity(cfg, setup, K, B=B, seed=300 + p, expect_fused=int(B > 1), threads=8)
 
 
 # other delays and move counts: m = 1 (nV = nu) and m = 3 (the one-QP-per-wave
@@ -628,12 +632,14 @@ def test_gpu_survey_config(plant, ctype, p, B, K):
                                                     ("par", "cent", 200, 8192, "rows"),
                                                     ("par", "coop", 50, 64, "split"),
                                                     ("par", "cent", 200, 1024, "split"),
-                                                    ("ser", "cent", 100, 64, "wave")])
+                                                    ("ser", "cent", 100, 64, "split"),
+                                                    ("ser", "cent", 100, 2048, "wave")])
 def test_gpu_build_auto_selects_kernel(plant, ctype, p, B, expect):
     """CMPC_BUILD_AUTO runs the four-QPs-per-wave kernel wherever its LDS fits
     and the batch gives it a wave per SIMD; below that the role-split kernel
     up to one QP per SIMD (SURVEY config 5: cent p = 200, 1 024 QPs), the
-    one-QP-per-wave kernel for ny = 4; DESIGN.md §3.0."""
+    one-QP-per-wave kernel between that and one row group per SIMD;
+    DESIGN.md §3.0."""
     _, setup, _, _ = setup_for(plant, ctype)
     cfg = cmpc.reference_config(plant, ctype, p=p)
     arr = cmpc.controller_arrays(cfg, setup)
@@ -645,7 +651,8 @@ def test_gpu_build_auto_selects_kernel(plant, ctype, p, B, expect):
 
 
 SPLIT_CASES = [("par", "cent", 200, None), ("par", "coop", 50, None), ("par", "ncoop", 20, None),
-               ("ser", "ncoop", 80, None), ("par", "coop", 50, (0, 10, 0, 25)), ("par", "cent", 60, (0, 45, 0, 45))]
+               ("ser", "ncoop", 80, None), ("par", "coop", 50, (0, 10, 0, 25)), ("par", "cent", 60, (0, 45, 0, 45)),
+               ("ser", "cent", 100, None), ("ser", "coop", 50, None), ("ser", "cent", 40, (0, 4, 0, 9))]
 
 
 @pytest.mark.gpu

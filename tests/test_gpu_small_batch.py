@@ -94,15 +94,17 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
 
 
 @pytest.mark.parametrize("ctype,B,solve,fused", [
-    ("cent", 16, cmpc.CMPC_SOLVE_ROWS, True), ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
-    ("coop", 1, cmpc.CMPC_SOLVE_LANE, True), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
+    ("cent", 16, cmpc.CMPC_SOLVE_ROWS, False), ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, True),
+    ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
+    ("coop", 1, cmpc.CMPC_SOLVE_LANE, False), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
     ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
 def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
     """CMPC_SOLVE_AUTO: the row solve kernel for small nV = 8 batches only;
-    CMPC_STEP_AUTO: cmpc_step fused below 16 384 QPs on the one-QP-per-wave
-    kernel under one row group per SIMD, and above it on the row kernel for
-    nV = 8 only (its fused step with the lane solver measured slower than the
-    two launches)."""
+    CMPC_STEP_AUTO: up to one QP per CU the role-split build and the
+    iterate kernel (two launches); cmpc_step fused from there below 16 384
+    QPs on the one-QP-per-wave kernel under one row group per SIMD, and above
+    it on the row kernel for nV = 8 only (its fused step with the lane solver
+    measured slower than the two launches)."""
     cfg = cmpc.reference_config("par", ctype, p=20)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", ctype))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
