@@ -166,16 +166,19 @@
 // lanes).  Even FUSE values record the working-set trace.  The QP is stored
 // either way (cmpc_download_qp).
 //
-// SPLIT (role split, small batches, ny <= 3, FUSE 0-2): two waves per QP in a
-// two-wave workgroup.  Wave 0 stages the record and runs the prologue and the
-// DPP chain of every step (P rows and the free response), storing the raw
-// Markov values into the delay lines and z into a two-block ring; wave 1 runs
-// the gather FMAs one block behind, reading those values, then the epilogue
-// (and the fused solve).  One workgroup barrier per block of up to U steps.
-// The same FMAs in the same order per lane: bit-identical to SPLIT = false,
-// with the two waves' instructions sharing a SIMD's issue slots (one wave per
-// SIMD issues an FP64 VALU about every 8 cycles).
-template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE, bool SPLIT = false>
+// SPLIT (role split, small batches): two waves per QP, SW waves per
+// workgroup (2: the split build kernel; 4: the one-launch control step, two
+// QPs).  The even wave of a pair stages the record and runs the prologue and
+// the DPP chain of every step (P rows and the free response; ny = 4: the
+// pre-pass too), storing the raw Markov values into the delay lines and z
+// into a two-block ring; the odd wave runs the gather FMAs one block behind,
+// reading those values, then the epilogue (and the fused solve).  One
+// workgroup barrier per block of up to U steps.  A pair uses two per-wave LDS
+// regions (the QP's, then the ring's).  The same FMAs in the same order per
+// lane: bit-identical to SPLIT = false, with the two waves' instructions
+// sharing a SIMD's issue slots (one wave per SIMD issues an FP64 VALU about
+// every 8 cycles).
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE, bool SPLIT = false, int SW = 2>
 __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int NV = NU * M;
@@ -190,13 +193,13 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   // pre-pass (every row simulating, row 3 storing z_r into per-output lines)
   // and the main pass has four P rows whose z lanes read those lines
   constexpr bool PRE = NY == 4;
-  static_assert(!SPLIT || FUSE <= 2, "role split: the row solver");
-  constexpr int WGW = SPLIT ? 2 : CMPC_BUILD_WAVES;  // waves per workgroup
-  constexpr int QPG = SPLIT ? 1 : CMPC_BUILD_WAVES;  // QPs per workgroup at a time
+  static_assert(!SPLIT || SW == 2 || SW == 4, "role split: two-wave pairs");
+  constexpr int WGW = SPLIT ? SW : CMPC_BUILD_WAVES;      // waves per workgroup
+  constexpr int QPG = SPLIT ? SW / 2 : CMPC_BUILD_WAVES;  // QPs per workgroup at a time
   const int lane = threadIdx.x & 63;
-  const int wave = SPLIT ? 0 : (threadIdx.x >> 6);   // QP slot of the workgroup
-  const bool wA = !SPLIT || (threadIdx.x >> 6) == 0;   // chain (and prologue) wave
-  const bool wB = !SPLIT || (threadIdx.x >> 6) == 1;   // gather (and epilogue) wave
+  const int wave = SPLIT ? (threadIdx.x >> 7) : (threadIdx.x >> 6);  // QP slot of the workgroup
+  const bool wA = !SPLIT || ((threadIdx.x >> 6) & 1) == 0;           // chain (and prologue) wave
+  const bool wB = !SPLIT || ((threadIdx.x >> 6) & 1) == 1;           // gather (and epilogue) wave
   const int row = lane >> 4, col = lane & 15;
   const int pp = P.p, S = P.S;
   const int nobs = P.nobs, rec_len = P.rec_len;
@@ -223,7 +226,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   double* lw_all = yl_all + S * P.yl_stride;
   double* uw_all = lw_all + S * NY * NY;
   double* zeros = uw_all + S * NU * NU;
-  double* recl = smem + P.lds_block + wave * P.lds_per_wave;
+  double* recl = smem + P.lds_block + (SPLIT ? 2 * wave : wave) * P.lds_per_wave;
   const int o_uold = rec_len, o_chat = o_uold + 8, o_kap = o_chat + NY * nobs;
   const int o_line = 0, o_w = P.w_off, o_zl = P.zs_off;
   // Delay parameters in registers (compile-time indices only): a runtime-
@@ -348,13 +351,17 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
   const uint64_t t0c = tlast, t0r = __builtin_amdgcn_s_memrealtime();
 #endif
-  // (SPLIT: one QP per workgroup, the launcher's grid covers the batch: no
-  // loop-carried state, so the fused solve has the registers of the build)
+  // (SPLIT: one QP per pair, the launcher's grid covers the batch: no
+  // loop-carried state, so the fused solve has the registers of the build;
+  // a pair past the batch runs once on the last QP, storing nothing, so that
+  // the workgroup's barriers match)
   bool first_qp = true;
-  for (; q < P.nqp; q = SPLIT ? P.nqp : q + nwaves) {
+  for (; q < P.nqp || (SPLIT && first_qp); q = SPLIT ? P.nqp : q + nwaves) {
+    const bool qv = q < P.nqp;
     if constexpr (SPLIT) {  // the previous QP's epilogue has read its LDS
       if (!first_qp) __syncthreads();
       first_qp = false;
+      if (!qv) q = P.nqp - 1;
     }
     CMPC_WT(5)  // back-edge
     {
@@ -653,7 +660,7 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) tot[k] += rr[k];
       }
-      if (row == 0 && col < NG) {
+      if (qv && row == 0 && col < NG) {
         double* out = P.qp + (size_t)q * P.qp_len;
         const double* uwt = uw_all + s * NU * NU;
         const int k2 = col / NUT, c2 = col - k2 * NUT;
@@ -690,19 +697,19 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // the totals are read before the scratch is written
       CMPC_WT(4)  // epilogue
-      if constexpr (SPLIT) {  // the factor in LDS (registers: two waves per SIMD)
+      if constexpr (SPLIT && SW == 2) {  // the factor in LDS (registers: two waves per SIMD)
         double* lsh = recl + P.lds_per_wave + (NY * 8 + 31) / 32 * 32 + row * N * N;
-        rows_solve_qp<N, NU, 0, FUSE == 2, false, true>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
+        rows_solve_qp<N, NU, 0, FUSE == 2, false, true>(P.sv, q, qv && row == 0, 0, col, rb, Hl, f_l, Gl,
                                                         red + NY * NG * NV + row * N * N, lsh);
       } else {
-        rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, row == 0, 0, col, rb, Hl, f_l, Gl,
+        rows_solve_qp<N, NU, 0, FUSE == 2, false>(P.sv, q, qv && row == 0, 0, col, rb, Hl, f_l, Gl,
                                                   red + NY * NG * NV + row * N * N);
       }
       __builtin_amdgcn_wave_barrier();
       CMPC_WT(1)  // fused solve
       continue;
     }
-    if (row == 0 && col < NG) {
+    if (qv && row == 0 && col < NG) {
       double tot[NV];
 #pragma unroll
       for (int k = 0; k < NV; ++k) tot[k] = acc[k];
@@ -738,9 +745,9 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     // the batch); the barrier's workgroup-scope release/acquire makes the
     // stores of the other waves visible to wave 0 (one CU, write-through L0)
     __syncthreads();
-    if (wave == 0 && lane < CMPC_BUILD_WAVES) {
+    if ((threadIdx.x >> 6) == 0 && lane < QPG) {
       constexpr int NVO = M * (NUT - NU);
-      const int ql = blockIdx.x * CMPC_BUILD_WAVES + lane;
+      const int ql = blockIdx.x * QPG + lane;
       const bool al = ql < P.nqp;
       const int qc = al ? ql : P.nqp - 1;
       const int sl = qc % S;
@@ -811,21 +818,26 @@ static size_t split_lds_bytes(const BuildParams& P, int ny) {
 // producer's table and rows overlay the build's dynamic LDS before the build
 // starts.
 // ---------------------------------------------------------------------------
-template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE>
+// SPLIT: the build as two role-split pairs (two QP slots per workgroup)
+template <int NS, int NY, int NUT, int NU, int M, int ND, int FUSE, bool SPLIT = false>
 __global__ __launch_bounds__(64 * CMPC_BUILD_WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void cmpc_control_step_kernel(ControlStepParams C) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int PLANT = NS == 11 ? CMPC_PLANT_PARALLEL : CMPC_PLANT_SERIAL;
+  constexpr int QPG = SPLIT ? CMPC_BUILD_WAVES / 2 : CMPC_BUILD_WAVES;  // QP slots per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the unit of this lane's DPP row in the producer and a-priori phases
+  // (rows past the workgroup's slots idle: an index past the batch)
+  const int unit = (lane >> 4) < QPG ? blockIdx.x * QPG + (lane >> 4) : 0x3fffffff;
   int* src = reinterpret_cast<int*>(smem);
   int* dmap = src + C.pr.S * C.pr.rec_len;
   cmpc_prod::produce_table<PLANT>(C.pr, src, dmap, threadIdx.x, 64 * CMPC_BUILD_WAVES);
   __syncthreads();
   if (wave == 0)
     cmpc_prod::produce_row<PLANT>(C.pr, smem + C.pr_off + (lane >> 4) * cmpc_prod::kScnLds, src, dmap,
-                                  blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+                                  unit, lane);
   __syncthreads();
-  build_wave_body<NS, NY, NUT, NU, M, ND, FUSE>(C.b);
+  build_wave_body<NS, NY, NUT, NU, M, ND, FUSE, SPLIT, CMPC_BUILD_WAVES>(C.b);
   // polled completion: each wave's result stores (du, status, nWSR in
   // page-locked host memory; waves 1-3 store theirs when the block has 2-4
   // centralized QPs) are released at system scope by the wave itself, before
@@ -834,7 +846,7 @@ void cmpc_control_step_kernel(ControlStepParams C) {
   if (C.done) __threadfence_system();
   __syncthreads();
   if (wave == 0) {
-    obs_prior_row<NS, NUT>(C.ob, blockIdx.x * CMPC_BUILD_WAVES + (lane >> 4), lane);
+    obs_prior_row<NS, NUT>(C.ob, unit, lane);
     // wave 0's a-priori stores before this release (a vector store, system
     // scope)
     if (C.done && lane == 0) __hip_atomic_store(C.done, C.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -843,7 +855,8 @@ void cmpc_control_step_kernel(ControlStepParams C) {
 
 #define CONTROL_CASE(NS_, NY_, NU_, M_, FUSE_)                                              \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {        \
-    auto k_ = cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_>;                      \
+    auto k_ = P.split ? cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_, true>        \
+                      : cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_>;            \
     if (lds > 64 * 1024)                                                                      \
       cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds);        \
     *solver = FUSE_ == 1 ? CMPC_SOLVE_ROWS : CMPC_SOLVE_LANE;                                 \
@@ -855,7 +868,8 @@ int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu,
                              int* solver) {
   hipStream_t s = (hipStream_t)stream;
   const BuildParams& P = C.b;
-  if (P.grid * CMPC_BUILD_WAVES < P.nqp || P.sv.trace) return -1;
+  // (P.split: two QP slots per workgroup, the role-split build)
+  if (P.grid * (P.split ? CMPC_BUILD_WAVES / 2 : CMPC_BUILD_WAVES) < P.nqp || P.sv.trace) return -1;
   if (C.pr.S != P.S || !C.pr.per_qp || !C.pr.obs_M) return -1;
   size_t lds = sizeof(double) * ((size_t)P.lds_block + (size_t)P.lds_per_wave * CMPC_BUILD_WAVES);
   lds = std::max(lds, sizeof(double) * ((size_t)C.pr_off + 4 * cmpc_prod::kScnLds));
@@ -866,7 +880,7 @@ int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu,
     CONTROL_CASE(10, 4, 4, 2, 1)  // serial centralized
     return -1;
   }
-  if (CMPC_BUILD_WAVES % P.S) return -1;
+  if ((P.split ? CMPC_BUILD_WAVES / 2 : CMPC_BUILD_WAVES) % P.S) return -1;
   CONTROL_CASE(11, 3, 2, 2, 3)  // parallel coop
   CONTROL_CASE(11, 2, 2, 2, 3)  // parallel ncoop
   CONTROL_CASE(10, 2, 2, 2, 3)  // serial ncoop
