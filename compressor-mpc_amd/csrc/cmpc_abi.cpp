@@ -1713,13 +1713,14 @@ int cmpc_last_solve_kernel(cmpc_ctx* c) {
 static int launch_solve(cmpc_ctx* c, const SolveParams& P, const char* who) {
   const int nV = c->L.nV, nu = c->d.nu, nVo = c->L.nVo;
   // AUTO: the row kernel for small batches of nV >= 6 QPs (centralized: the
-  // lane kernel's nV = 8 solve is one long dependency chain per lane, 25 us
-  // for one solve of 1 024 QPs against 18 us in rows, tools/time_small.py);
-  // at nV = 4 the lane kernel is faster at every batch size (K = 9 on 8 192
-  // QPs: 15.3 vs 21.2 us: the row gathers cost more than the 4 x 4 products
-  // they spread)
-  const bool want_rows = c->solve_variant == CMPC_SOLVE_ROWS ||
-                         (c->solve_variant == CMPC_SOLVE_AUTO && c->nqp < CMPC_SOLVE_ROWS_MAX_QP && nV >= 6);
+  // lane kernel's nV = 8 solve is one long dependency chain per lane, 17 us
+  // for one solve of 1 024 QPs against 9 us in rows, tools/time_small.py);
+  // at nV = 4 up to one QP per SIMD (K = 9: 7.7-7.8 vs 9.7-9.9 us from 2 to
+  // 1 024 QPs), the lane kernel above (8 192 QPs: 9.8 vs 16.1 us;
+  // profiles/r5k_small_batch.txt)
+  if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const bool rows_small = nV >= 6 ? c->nqp < CMPC_SOLVE_ROWS_MAX_QP : c->nqp <= 4 * std::max(c->cus, 1);
+  const bool want_rows = c->solve_variant == CMPC_SOLVE_ROWS || (c->solve_variant == CMPC_SOLVE_AUTO && rows_small);
   if (want_rows && cmpc_launch_solve_rows(P, nV, nu, nVo, c->stream) == 0) {
     c->last_solve = CMPC_SOLVE_ROWS;
     return 0;
@@ -1922,11 +1923,13 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   // solver of wave 0 after a workgroup barrier for S = 2, 4), the row kernel
   // from one row group per SIMD up to 16 384 QPs (config 2)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  // (up to one QP per CU AUTO runs the role-split build and the iterate
-  // kernel instead: cent-ser B = 1 21.8 vs 24.4 us, coop-par B = 1 19.3 vs
-  // 19.9 us; config 5, 1 024 QPs, stays fused: 37.2 vs 38.4 us with the move,
-  // profiles/r5j_split_step_ab.txt)
-  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && c->nqp > std::max(c->cus, 1);
+  // (AUTO fuses nV >= 6 steps above one QP per CU only: below it the
+  // role-split build and the iterate kernel are faster (cent-ser B = 1 21.8 vs
+  // 24.4 us), config 5 (1 024 QPs) fused 37.2 vs 38.4 us with the move; nV = 4
+  // steps are two launches at every size (coop-par 1 024 QPs 17.8 vs 18.6 us,
+  // config 2 26.4 vs 54.1 us; profiles/r5j_split_step_ab.txt,
+  // profiles/r5k_small_batch.txt))
+  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && c->nqp > std::max(c->cus, 1) && c->L.nV >= 6;
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
                     (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);

@@ -163,8 +163,10 @@
 // stores); 3/4 (S divides 4, nV <= 4): the workgroup's QPs, built and stored
 // one per wave, are solved one per lane of wave 0 after a workgroup barrier
 // (lane_solve.h; a scenario's sub-controllers are adjacent waves, so adjacent
-// lanes).  Even FUSE values record the working-set trace.  The QP is stored
-// either way (cmpc_download_qp).
+// lanes); 5 (the same, nV <= 4): solved one per DPP row of wave 0 by the row
+// solver (solve_rows.h; faster than the lane solver at a few QPs).  Even FUSE
+// values record the working-set trace.  The QP is stored either way
+// (cmpc_download_qp).
 //
 // SPLIT (role split, small batches): two waves per QP, SW waves per
 // workgroup (2: the split build kernel; 4: the one-launch control step, two
@@ -745,8 +747,33 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
     // the batch); the barrier's workgroup-scope release/acquire makes the
     // stores of the other waves visible to wave 0 (one CU, write-through L0)
     __syncthreads();
-    if ((threadIdx.x >> 6) == 0 && lane < QPG) {
-      constexpr int NVO = M * (NUT - NU);
+    constexpr int NVO = M * (NUT - NU);
+    if constexpr (FUSE == 5) {
+      // the row solver: wave 0's DPP row r solves the workgroup's QP r (a
+      // scenario's sub-controllers in adjacent rows), as the row iterate
+      // kernel does (solve_rows.hip), in the build's LDS (its N x N scratch
+      // per row after the lines, which are dead)
+      static_assert(QPG <= 4, "one QP per DPP row of wave 0");
+      if ((threadIdx.x >> 6) == 0) {
+        constexpr int NVOA = NVO > 0 ? NVO : 1;
+        const int l = col;
+        const int ql = blockIdx.x * QPG + row;
+        const bool al = row < QPG && ql < P.nqp;
+        const int qc = ql < P.nqp ? ql : P.nqp - 1;
+        const int sl = qc % S;
+        const bool own = l < NV;
+        const int lr = own ? l : NV - 1;
+        const double* qr = P.qp + (size_t)qc * P.qp_len;
+        double Hl[NV], Gl[NVOA];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) Hl[c] = own ? qr[lr * NV + c] : 0.0;
+        const double f_l = own ? qr[NV * NV + lr] : 0.0;
+#pragma unroll
+        for (int c = 0; c < NVOA; ++c) Gl[c] = (NVO > 0 && own) ? qr[NV * NV + NV + lr * NVO + c] : 0.0;
+        rows_solve_qp<NV, NU, NVO, false, false>(P.sv, qc, al, sl, l, (lane & ~15) - 16 * sl, Hl, f_l, Gl,
+                                                 smem + P.lds_block + row * NV * NV);
+      }
+    } else if ((threadIdx.x >> 6) == 0 && lane < QPG) {
       const int ql = blockIdx.x * QPG + lane;
       const bool al = ql < P.nqp;
       const int qc = al ? ql : P.nqp - 1;
@@ -853,13 +880,16 @@ void cmpc_control_step_kernel(ControlStepParams C) {
   }
 }
 
-#define CONTROL_CASE(NS_, NY_, NU_, M_, FUSE_)                                              \
+// FUSE_: the solve after the build; FUSES_: the same with the role-split
+// build (up to one QP per CU: the coop row solver, faster there)
+#define CONTROL_CASE(NS_, NY_, NU_, M_, FUSE_, FUSES_)                                      \
   if (ns == NS_ && ny == NY_ && nu == NU_ && m == M_ && P.nd == 2 && P.nu_tot == 4) {        \
-    auto k_ = P.split ? cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_, true>        \
+    auto k_ = P.split ? cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSES_, true>       \
                       : cmpc_control_step_kernel<NS_, NY_, 4, NU_, M_, 2, FUSE_>;            \
     if (lds > 64 * 1024)                                                                      \
       cmpc_allow_lds(reinterpret_cast<const void*>(k_), lds);        \
-    *solver = FUSE_ == 1 ? CMPC_SOLVE_ROWS : CMPC_SOLVE_LANE;                                 \
+    const int f_ = P.split ? FUSES_ : FUSE_;                                                  \
+    *solver = (f_ == 1 || f_ == 5) ? CMPC_SOLVE_ROWS : CMPC_SOLVE_LANE;                       \
     cmpc_launch(k_, dim3(std::max(1, P.grid)), dim3(64 * CMPC_BUILD_WAVES), lds, s, C);      \
     return 0;                                                                                 \
   }
@@ -876,15 +906,15 @@ int cmpc_launch_control_step(const ControlStepParams& C, int ns, int ny, int nu,
   if (lds > 160 * 1024) return -1;
   if (P.S == 1) {
     if (P.lds_per_wave < ny * (m * 4 + 1) * (nu * m) + 4 * (nu * m) * (nu * m)) return -1;
-    CONTROL_CASE(11, 3, 4, 2, 1)  // parallel centralized
-    CONTROL_CASE(10, 4, 4, 2, 1)  // serial centralized
+    CONTROL_CASE(11, 3, 4, 2, 1, 1)  // parallel centralized
+    CONTROL_CASE(10, 4, 4, 2, 1, 1)  // serial centralized
     return -1;
   }
   if ((P.split ? CMPC_BUILD_WAVES / 2 : CMPC_BUILD_WAVES) % P.S) return -1;
-  CONTROL_CASE(11, 3, 2, 2, 3)  // parallel coop
-  CONTROL_CASE(11, 2, 2, 2, 3)  // parallel ncoop
-  CONTROL_CASE(10, 2, 2, 2, 3)  // serial ncoop
-  CONTROL_CASE(10, 4, 2, 2, 3)  // serial coop
+  CONTROL_CASE(11, 3, 2, 2, 3, 5)  // parallel coop
+  CONTROL_CASE(11, 2, 2, 2, 3, 5)  // parallel ncoop
+  CONTROL_CASE(10, 2, 2, 2, 3, 5)  // serial ncoop
+  CONTROL_CASE(10, 4, 2, 2, 3, 5)  // serial coop
   return -1;
 }
 

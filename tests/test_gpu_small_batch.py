@@ -96,15 +96,15 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
 @pytest.mark.parametrize("ctype,B,solve,fused", [
     ("cent", 16, cmpc.CMPC_SOLVE_ROWS, False), ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, True),
     ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
-    ("coop", 1, cmpc.CMPC_SOLVE_LANE, False), ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
+    ("coop", 1, cmpc.CMPC_SOLVE_ROWS, False), ("coop", 512, cmpc.CMPC_SOLVE_ROWS, False),
+    ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
     ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
 def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
-    """CMPC_SOLVE_AUTO: the row solve kernel for small nV = 8 batches only;
-    CMPC_STEP_AUTO: up to one QP per CU the role-split build and the
-    iterate kernel (two launches); cmpc_step fused from there below 16 384
-    QPs on the one-QP-per-wave kernel under one row group per SIMD, and above
-    it on the row kernel for nV = 8 only (its fused step with the lane solver
-    measured slower than the two launches)."""
+    """CMPC_SOLVE_AUTO: the row solve kernel for nV = 8 batches below 16 384
+    QPs and nV = 4 batches up to one QP per SIMD; CMPC_STEP_AUTO: nV = 8
+    steps fused above one QP per CU and below 16 384 QPs (the one-QP-per-wave
+    kernel under one row group per SIMD, the row kernel above), every other
+    step the build and the iterate kernel (two launches)."""
     cfg = cmpc.reference_config("par", ctype, p=20)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", ctype))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)

@@ -15,6 +15,8 @@ from cmpc.synthetic import synthetic_batch  # noqa: E402
 CONFIGS = {  # name: (plant, controller, p, B scenarios, K)
     "c5": ("par", "cent", 200, 1024, 1),
     "c2": ("par", "coop", 20, 4096, 9),
+    "c2q256": ("par", "coop", 20, 128, 9),
+    "c2q1k": ("par", "coop", 20, 512, 9),
     "b1": ("par", "coop", 50, 1, 9),
     "c1b1": ("ser", "cent", 100, 1, 1),
     "c3": ("par", "ncoop", 50, 65536, 1),
