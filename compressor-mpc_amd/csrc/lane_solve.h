@@ -86,7 +86,9 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
   for (int k = 0; k < P.K; ++k) {
 #if CMPC_SOLVE_PRIO
     {  // fair progress of the SIMD's waves (cf. build_rows.hip)
-      const int level = 3 - (4 * k) / (P.K > 0 ? P.K : 1);
+      // 3 - floor(4 k / K) by comparisons (a runtime integer division is a
+      // long scalar sequence on this target, once per iteration)
+      const int level = 3 - (4 * k >= P.K) - (4 * k >= 2 * P.K) - (4 * k >= 3 * P.K);
       if (level <= 0) __builtin_amdgcn_s_setprio(0);
       else if (level == 1) __builtin_amdgcn_s_setprio(1);
       else if (level == 2) __builtin_amdgcn_s_setprio(2);
