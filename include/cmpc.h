@@ -181,7 +181,8 @@ int cmpc_last_build_kernel(cmpc_ctx* ctx);
  * CMPC_SOLVE_LANE one QP per lane (large batches); CMPC_SOLVE_ROWS one QP per
  * 16-lane DPP row, its H^-1 and matrix-vector products spread over the row
  * (batches that leave most SIMDs idle; needs S | 4); CMPC_SOLVE_AUTO
- * (default) rows below CMPC_SOLVE_ROWS_MAX_QP QPs where available. */
+ * (default) rows for nV >= 6 below CMPC_SOLVE_ROWS_MAX_QP QPs and for smaller
+ * nV up to one QP per SIMD, where available. */
 #define CMPC_SOLVE_AUTO 0
 #define CMPC_SOLVE_LANE 1
 #define CMPC_SOLVE_ROWS 2
@@ -192,8 +193,9 @@ int cmpc_last_solve_kernel(cmpc_ctx* ctx);
  * the QPs it built, H, f, G handed over in registers; the same results bit
  * for bit as cmpc_build + cmpc_iterate with the row solve kernel):
  * CMPC_STEP_SPLIT two launches; CMPC_STEP_FUSED one (an error where no fused
- * kernel exists for the dimensions); CMPC_STEP_AUTO (default) fused below
- * CMPC_SOLVE_ROWS_MAX_QP QPs where available. */
+ * kernel exists for the dimensions); CMPC_STEP_AUTO (default) fused for
+ * nV >= 6 from one QP per CU up to CMPC_SOLVE_ROWS_MAX_QP QPs, two launches
+ * otherwise (measured faster there: DESIGN.md §3.0). */
 #define CMPC_STEP_AUTO 0
 #define CMPC_STEP_SPLIT 1
 #define CMPC_STEP_FUSED 2
