@@ -334,7 +334,9 @@ def time_config(name, plant, ctype, p, B, K, local, settle_seconds, steps, NB=2,
             ctx.build()
         bms, bn = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
         ctx.enable_timing(False)
-        bkern = "cmpc_build_rows_kernel" if ctx.last_build_kernel() == cmpc.CMPC_BUILD_ROWS else "cmpc_build_kernel"
+        bkern = {cmpc.CMPC_BUILD_ROWS: "cmpc_build_rows_kernel",
+                 getattr(cmpc, "CMPC_BUILD_SPLIT", -1): "cmpc_build_split_kernel"}.get(ctx.last_build_kernel(),
+                                                                                     "cmpc_build_kernel")
         L = ctx.layout
         restore()
         changes, _ = traced_changes(ctx, K, bind, range(i, i + steps))  # the timed steps, replayed

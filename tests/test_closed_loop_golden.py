@@ -188,3 +188,16 @@ def test_gpu_closed_loop_scenarios_match_oracle(name):
             yo = ora.step()
             np.testing.assert_allclose(u[k, b], ora.u_ctrl, rtol=2e-6, atol=1e-10, err_msg=f"u {b} {k}")
             np.testing.assert_allclose(y[k, b], yo, rtol=2e-6, atol=1e-10, err_msg=f"y {b} {k}")
+
+
+def test_six_digit_rows_tie_rule():
+    """golden_cases.six_digit_rows: equal %.6g prints match; a value within
+    1e-9 of a rounding boundary may print as either neighbour (a tie); one
+    unit off elsewhere, or two units at a boundary, is a difference."""
+    got = np.array([[-8.995135e-08, 1.0], [1.234565e-3, 2.0], [1.2345e-3, 0.5]])
+    ref = np.array([[-8.99513e-08, 1.0], [1.23457e-3, 2.0], [1.2346e-3, 0.5]])
+    bad, tie = GC.six_digit_rows(got, ref)
+    assert list(tie) == [1] and list(bad) == [2]  # (row 0 prints equal)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457]) == (False, True)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23458]) == (False, False)
+    assert GC.six_digit_strings_ok(["0", "2.5"], [1e-13, 2.5]) == (True, False)
