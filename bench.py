@@ -1033,6 +1033,11 @@ def main():
                                      "mean over a traced replay of all the timed steps from the same "
                                      "states (CMPC_TRACE counts); per_qp_step = per step / (B S)"),
         "recorded_run": recorded,
+        # the recorded run's solver load beside the synthetic headline's
+        # working_set_changes_per_qp_step (the synthetic load is the higher
+        # one, so no variant calibrated to the recorded rate is reported)
+        "recorded_run_working_set_changes_per_qp_step": (
+            recorded.get("working_set_changes_per_qp_step") if isinstance(recorded, dict) else None),
         "harder_qp": harder,
         "configs": configs,
         "closed_loop_device_resident": closed,

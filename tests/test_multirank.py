@@ -253,3 +253,6 @@ def test_gpu_bench_force_dist_single_rank():
     assert d["qp_status_ok_fraction"] == 1.0
     assert d["coupled"]["exchange"].startswith("RCCL")
     assert d["coupled"]["qp_status_ok_fraction"] == 1.0
+    # the recorded run's solver load beside the synthetic one
+    assert d["recorded_run_working_set_changes_per_qp_step"] == d["recorded_run"]["working_set_changes_per_qp_step"]
+    assert d["recorded_run_working_set_changes_per_qp_step"] < d["working_set_changes_per_qp_step"]
