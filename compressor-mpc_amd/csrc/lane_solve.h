@@ -13,6 +13,9 @@
 #include "cmpc_internal.h"
 #include "qp_solver.h"
 
+#ifndef CMPC_SOLVE_XU_LDS
+#define CMPC_SOLVE_XU_LDS 1  // x_u0 in H^-1's unused LDS slots (0: registers)
+#endif
 #ifndef CMPC_SOLVE_PRIO
 #define CMPC_SOLVE_PRIO 1  // priority by Jacobi-iteration progress (iterate 0.049 -> 0.047 ms)
 #endif
@@ -81,6 +84,20 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
     if constexpr (UIN) return UStrided<NVOA, GSTRIDE>{gb};
     else return URegs<N, NVOA>{Ur};
   }();
+  // x_u0 into H^-1's unused LDS slots where H^-1 lives in LDS (its 4
+  // registers were spilled to scratch across the iterations and reloaded
+  // at every map build)
+  auto xu0_of = [&]() -> decltype(auto) {
+    if constexpr (CMPC_SOLVE_XU_LDS && !std::is_same_v<HS, HinvRegs<N>> && N >= 3) {
+      XuStrided<N, HS::kStride> xs{hsh};
+#pragma unroll
+      for (int r = 0; r < N; ++r) xs.set(r, xu0[r]);
+      return xs;
+    } else {
+      return (xu0);
+    }
+  };
+  decltype(auto) xa = xu0_of();
   JMap<N, NVO> mp;
   mp.ws = kWsInvalid;
   for (int k = 0; k < P.K; ++k) {
@@ -135,7 +152,7 @@ __device__ __forceinline__ void lane_solve_qp(const SolveParams& P, int q, bool 
       }
     }
     // f_k = f + (Su_other du_other)' W Su = f + G du_other, in the map form
-    qp_solve_map<TRACE, N, NVO>(qp, pd, tol_d, xu0, U, dother, ws, CMPC_NWSR_MAX, x, o, mp);
+    qp_solve_map<TRACE, N, NVO>(qp, pd, tol_d, xa, U, dother, ws, CMPC_NWSR_MAX, x, o, mp);
     ws = o.ws;
 #pragma unroll
     for (int a = 0; a < N; ++a) dprev[a] = x[a];

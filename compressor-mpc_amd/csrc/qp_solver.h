@@ -51,11 +51,33 @@ struct HinvRegs {
 template <int N, int STRIDE>
 struct HinvStrided {
   static constexpr bool kColumns = true;  // H^-1 nu by column reads (runtime addresses)
+  static constexpr int kStride = STRIDE;
   double* p;
   CMPC_HD double operator()(int r, int c) const { return r <= c ? p[(r * N + c) * STRIDE] : p[(c * N + r) * STRIDE]; }
   CMPC_HD void set(int r, int c, double v) {
     if (r <= c) p[(r * N + c) * STRIDE] = v;
   }
+};
+
+// x_u0 = -H^-1 f of the map form in the strictly lower triangle that
+// HinvStrided leaves unused (entry r in the r-th slot (i, j), i > j, in row
+// order; N >= 3): read only to build a map and to leave one, so it holds no
+// registers across the Jacobi iterations
+template <int N, int STRIDE>
+struct XuStrided {
+  static_assert(N >= 3, "needs N lower-triangle slots");
+  double* p;
+  static constexpr CMPC_HD int slot(int r) {
+    int n = 0;
+    for (int i = 1; i < N; ++i)
+      for (int j = 0; j < i; ++j) {
+        if (n == r) return i * N + j;
+        ++n;
+      }
+    return -1;
+  }
+  CMPC_HD double operator[](int r) const { return p[slot(r) * STRIDE]; }
+  CMPC_HD void set(int r, double v) { p[slot(r) * STRIDE] = v; }
 };
 
 // NB = stored bound entries: N (general), or NU when the bounds repeat every
@@ -754,9 +776,12 @@ struct UStrided {
 // explicit normal is formed once and serves all 1 + NVO right-hand sides
 // (N' x_u0 and N' U's columns: FMAs with 0 / +-1 coefficients, exact, the
 // oracle's nu_dot values).
-template <int N, int NVO, int NU, int NB, class HS, bool SN, class LS, class UA>
-CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN, LS>& W, const double (&xu0)[N],
+template <int N, int NVO, int NU, int NB, class HS, bool SN, class LS, class XU, class UA>
+CMPC_HD void jmap_build(const Qp<N, NU, NB, HS>& q, const WSet<N, SN, LS>& W, const XU& xu0v,
                         const UA& U, JMap<N, NVO>& mp) {
+  double xu0[N];  // (an array, or XuStrided in LDS)
+#pragma unroll
+  for (int r = 0; r < N; ++r) xu0[r] = xu0v[r];
   constexpr int NVOA = JMap<N, NVO>::NVOA;
   double rhs0[N], rc[NVOA][N];
 #pragma unroll
@@ -823,8 +848,8 @@ CMPC_HD uint32_t wset_word(const WSet<N, SN, LS>& W) {
 // constraint) touches only the map; otherwise the working set and its fresh
 // factor are rebuilt from ws_in (the same values as when the map was built)
 // and the solve continues as the plain one.
-template <bool TRACE, int N, int NVO, int NU, int NB, class HS, class UA>
-CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const double (&xu0)[N],
+template <bool TRACE, int N, int NVO, int NU, int NB, class HS, class XU, class UA>
+CMPC_HD void qp_solve_map(const Qp<N, NU, NB, HS>& q, bool pd, double tol_d, const XU& xu0,
                           const UA& U, const double (&d)[JMap<N, NVO>::NVOA], uint32_t ws_in, int max_chg,
                           double (&x)[N], QpOut& o, JMap<N, NVO>& mp) {
   WSet<N> W;
