@@ -95,3 +95,34 @@ def test_gpu_step_on_produced_records():
     du_h, st_h, _ = run(lambda c: c.upload_lin(recs))
     assert np.array_equal(st_d, st_h)
     np.testing.assert_allclose(du_d, du_h, rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_gpu_producer_strided_batch():
+    """A batch larger than the producer's resident workgroups (each wave then
+    produces several groups of four scenarios, CMPC_PRODUCE_LOOP): every record
+    is written (its controlled-output tail is the scenario's y, copied exactly)
+    and sampled records, the last ones among them, equal the host producer's."""
+    import torch
+    cfg = cmpc.reference_config("par", "coop", p=50)
+    B = 40_003  # 10 001 groups of four scenarios, the last one partial
+    x, u, y = operating_points(cfg, B, seed=13)
+    dims = CmpcDims.from_config(cfg, B)
+    L = cmpc.layout_of(dims)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+    tx, tu, ty = dev(x), dev(u), dev(y)
+    with cmpc.Context(cfg, B, device=0) as ctx:
+        ctx.upload_lin(np.full((B * cfg.S, L.rec_len), np.nan))
+        ctx.produce_lin(tx.data_ptr(), tu.data_ptr(), ty.data_ptr())
+        got = ctx.download_lin()
+    assert np.isfinite(got).all()
+    for s in range(cfg.S):
+        np.testing.assert_array_equal(got[s::cfg.S, L.off_y:L.off_y + cfg.ny], y[:, cfg.out_idx[s]])
+    rng = np.random.default_rng(5)
+    sample = np.concatenate([rng.choice(B, 200, replace=False), np.arange(B - 9, B)])
+    for b in sample:
+        for s in range(cfg.S):
+            ref = np.zeros(L.rec_len)
+            cmpc.plant_lin_record(cfg, dims, s, x[b], u[b], out=ref)
+            ref[L.off_y:L.off_y + cfg.ny] = y[b][cfg.out_idx[s]]
+            np.testing.assert_allclose(got[b * cfg.S + s], ref, rtol=1e-13, atol=1e-300)
