@@ -14,8 +14,16 @@ using namespace cmpc_prod;
 // (One group per wave, the phases of the resident waves stayed in step: the
 // compute (53 us at 65 536 scenarios) and the record stores (51 us, near the
 // write bandwidth) added up, profiles/r5u_produce_loop_ab/.)
+#ifndef CMPC_PRODUCE_WPE
+#define CMPC_PRODUCE_WPE 0  // waves per SIMD the registers are allocated for (0: the compiler's choice, 2)
+#endif
+#if CMPC_PRODUCE_WPE
+#define CMPC_PRODUCE_ATTR __attribute__((amdgpu_waves_per_eu(CMPC_PRODUCE_WPE, CMPC_PRODUCE_WPE)))
+#else
+#define CMPC_PRODUCE_ATTR
+#endif
 template <int PLANT>
-__global__ __launch_bounds__(64 * kWaves) void cmpc_produce_kernel(ProduceParams P) {
+__global__ __launch_bounds__(64 * kWaves) CMPC_PRODUCE_ATTR void cmpc_produce_kernel(ProduceParams P) {
   __shared__ double lds[kWaves * kSpw * kScnLds];
   extern __shared__ int src[];  // S x rec_len, then naug (dynamic, cmpc_launch_produce)
   int* dmap = src + P.S * P.rec_len;  // observer tail entry -> its position in the dx row
