@@ -98,39 +98,12 @@ __device__ __forceinline__ void produce_table(const ProduceParams& P, int* src, 
   }
 }
 
-// The unit's inputs that produce_row reads from HBM (lane l of the row: x
-// entry l, u_full entry l, output l).  On gfx9 loads and stores share one
-// memory counter, so a load issued after a group's record stores waits for
-// them: the looping producer kernel loads the next group's inputs before this
-// group's stores (xu_next), and the outputs are loaded before any store.
-struct ProduceInputs {
-  double x, u, y;
-};
-template <int PLANT>
-__device__ __forceinline__ ProduceInputs produce_inputs(const ProduceParams& P, int unit, int lane) {
-  constexpr int ns = PLANT == CMPC_PLANT_PARALLEL ? 11 : 10;
-  constexpr int ni = PLANT == CMPC_PLANT_PARALLEL ? 9 : 8;
-  const int l = lane % kLanes;
-  const bool valid = unit < (P.per_qp ? P.B * P.S : P.B);
-  const int b = P.per_qp ? unit / P.S : unit;
-  const bool post = P.per_qp && P.obs_M;  // (x from the a-posteriori update)
-  ProduceInputs in;
-  in.x = (valid && l < ns && !post) ? (P.per_qp ? P.x[(size_t)unit * P.x_stride + l] : P.x[(size_t)b * ns + l])
-                                    : 0.0;
-  in.u = (valid && l < ni) ? P.u_full[(size_t)b * ni + l] : 0.0;
-  in.y = (valid && l < P.n_outputs) ? P.y[(size_t)b * P.n_outputs + l] : 0.0;
-  return in;
-}
-
 // One unit (scenario, or QP slot in per-QP mode) on one 16-lane DPP row of
 // this wave: w = the row's kScnLds-double LDS region, lane = lane in the wave.
-// Every lane of the wave calls it (wave barriers inside).  in: the unit's
-// inputs loaded ahead (or null: loaded here); next: filled with next_unit's
-// inputs before the record stores (or null).
+// Every lane of the wave calls it (wave barriers inside).
 template <int PLANT>
 __device__ __forceinline__ void produce_row(const ProduceParams& P, double* w, const int* src, const int* dmap,
-                                            int unit, int lane, const ProduceInputs* in = nullptr,
-                                            ProduceInputs* next = nullptr, int next_unit = 0) {
+                                            int unit, int lane) {
   const int g = lane / kLanes, l = lane - g * kLanes;  // unit row, lane in row
   const bool valid = unit < (P.per_qp ? P.B * P.S : P.B);  // (rows past the batch idle
                                                            //  but keep the wave's syncs)
@@ -151,7 +124,6 @@ __device__ __forceinline__ void produce_row(const ProduceParams& P, double* w, c
   // then the linearisation at the updated x_hat.  The updated disturbance
   // states of dx reach the record's observer tail from registers (dnd).
   const bool post = P.per_qp && P.obs_M;
-  const ProduceInputs inp = in ? *in : produce_inputs<PLANT>(P, unit, lane);
   double xq = 0.0, dnd = 0.0;
   if (post) {
     constexpr int NO = 4, NOBS = ns + NO;  // disturbance states = outputs (C = [C_plant | I])
@@ -190,8 +162,9 @@ __device__ __forceinline__ void produce_row(const ProduceParams& P, double* w, c
       if (l < NO) yo[l] = yl;
     }
   }
-  if (valid && l < ns) xs[l] = post ? xq : inp.x;
-  if (valid && l < ni) us[l] = inp.u;
+  if (valid && l < ns)
+    xs[l] = post ? xq : P.per_qp ? P.x[(size_t)unit * P.x_stride + l] : P.x[(size_t)b * ns + l];
+  if (valid && l < ni) us[l] = P.u_full[(size_t)b * ni + l];
   for (int e = l; e < ns * ns; e += kLanes) A[e] = 0.0;  // the row clears, its lane 0
   for (int e = l; e < ns * 4; e += kLanes) {             // writes the nonzeros
     Bc[e] = 0.0;
@@ -254,7 +227,6 @@ __device__ __forceinline__ void produce_row(const ProduceParams& P, double* w, c
     }
     WAVE_SYNC();
   }
-  if (next) *next = produce_inputs<PLANT>(P, next_unit, lane);
   if (!valid || PRODUCE_EXP == 3) return;
 
   // the observer's next a-posteriori step reads this linearisation's C
@@ -299,13 +271,9 @@ __device__ __forceinline__ void produce_row(const ProduceParams& P, double* w, c
       for (int u = 0; u < kU; ++u)
         if (e0 + u * kLanes < P.naug) rec[P.off_x + e0 + u * kLanes] = v[u];
     }
-    // y (kY - o: output o, from lane o of the row's inputs) or padding
-    // (kZero); the loop is the wave's (the shuffle reads other lanes)
-    for (int e0 = P.off_x + P.naug; e0 < P.rec_len; e0 += kLanes) {
-      const int e = e0 + l;
-      const int t = e < P.rec_len ? srow[e] : kZero;
-      const double yv = __shfl(inp.y, (lane & ~(kLanes - 1)) + (t == kZero ? 0 : kY - t), 64);
-      if (e < P.rec_len) rec[e] = (t == kZero) ? 0.0 : yv;
+    for (int e = P.off_x + P.naug + l; e < P.rec_len; e += kLanes) {
+      const int t = srow[e];  // y (kY - o) or padding (kZero)
+      rec[e] = (t == kZero) ? 0.0 : P.y[(size_t)b * P.n_outputs + (kY - t)];
     }
   }
 }
