@@ -99,10 +99,10 @@ def test_gpu_step_on_produced_records():
 
 @pytest.mark.gpu
 def test_gpu_producer_strided_batch():
-    """A batch larger than the producer's resident workgroups (each wave then
-    produces several groups of four scenarios, CMPC_PRODUCE_LOOP): every record
-    is written (its controlled-output tail is the scenario's y, copied exactly)
-    and sampled records, the last ones among them, equal the host producer's."""
+    """A batch of several rounds of resident workgroups with a partial last
+    group: every record is written (its controlled-output tail is the
+    scenario's y, copied exactly) and sampled records, the last ones among
+    them, equal the host producer's."""
     import torch
     cfg = cmpc.reference_config("par", "coop", p=50)
     B = 40_003  # 10 001 groups of four scenarios, the last one partial
