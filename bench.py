@@ -20,10 +20,14 @@ controller hot-starts its own QProblem.
 
 Multi-GPU: one process per GPU (torch.distributed.run), scenarios sharded
 across ranks with no data-path collective (weak scaling); the barrier and
-the max-over-ranks of the elapsed time use torch.distributed (RCCL).  The
-`coupled` section beside the metric runs SURVEY config 4 on the same ranks:
-S_local = 8 sub-controllers per GPU of S_total = 8 x world per scenario, the
-plans all-gathered over RCCL once per Jacobi iteration.
+the max-over-ranks of the elapsed time use torch.distributed (RCCL).  A plain
+`python bench.py --gpus N` (no launcher environment) starts the N ranks itself:
+a torch.distributed.run child process, rank 0's line relayed, the child's exit
+code returned; fewer than N visible GPUs is an error.  The `coupled` section
+beside the metric runs SURVEY config 4 on the same ranks: S_local = 8
+sub-controllers per GPU of S_total = 8 x world per scenario, the plans
+all-gathered over RCCL once per Jacobi iteration; `coupled_s64` runs config
+4's own 64-sub-controller system at every world size (64 / world per GPU).
 
 Prints ONE JSON line (rank 0).
 """
@@ -452,6 +456,61 @@ def run_configs(local, settle_seconds, steps, with_cpp=True, markers=False):
     return configs
 
 
+SELF_LAUNCH_ENV = "CMPC_BENCH_SELF_LAUNCHED"
+
+
+def launch_plan(gpus: int, backend: str, env, device_count):
+    """How `bench.py --gpus N` runs.
+
+    Returns ("here", None) when this process is a rank already (a launcher set
+    WORLD_SIZE) or N = 1, or ("spawn", N) when the parent must start N ranks
+    itself: the driver's plain `python3 bench.py --gpus N` then measures N GPUs
+    instead of one.  Raises SystemExit (non-zero) when the ranks cannot match
+    the request: WORLD_SIZE differs from --gpus, or fewer than N devices are
+    visible for RCCL (one rank per GPU; gloo rehearsals may share a GPU).
+    device_count is a callable, asked only when needed; the caller passes one
+    that does not initialise the GPU (torch.cuda.device_count() on this image)."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={gpus}: the launcher and the "
+                             "request disagree")
+        return "here", None
+    if gpus <= 1:
+        return "here", None
+    if backend == "nccl":
+        n = device_count()
+        if n < gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} needs {gpus} visible GPUs for one RCCL rank per "
+                             f"GPU, {n} visible")
+    return "spawn", gpus
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, script=None) -> int:
+    """Start `python -m torch.distributed.run --nproc-per-node n bench.py argv`
+    as a child process (never exec: this process stays the parent), relay its
+    stdout (rank 0's JSON line) and return its exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env[SELF_LAUNCH_ENV] = "1"
+    log("bench.py: starting " + " ".join(cmd[1:]))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -470,6 +529,10 @@ def main():
     ap.add_argument("--headline-only", action="store_true",
                     help="only the metric's steps (no K = 1, closed-loop, coupled or CPU sections): "
                          "profiler runs, so that every build launch in the trace is a headline one")
+    ap.add_argument("--markers", action="store_true",
+                    help="a torch.cuda._sleep launch before and after the timed steps and before and "
+                         "after the iterate's event pass, so that a kernel trace of the run can be cut "
+                         "to exactly those launches (tools/headline_pass_stats.py)")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--configs-only", action="store_true",
                     help="only the SURVEY-config section's GPU configs (2, 3, 5), one JSON line: "
@@ -489,13 +552,23 @@ def main():
                          "on a one-GPU box)")
     args = ap.parse_args()
 
+    def device_count():
+        import torch  # device_count() does not initialise the GPU (no HIP context)
+        return torch.cuda.device_count()
+
+    mode, n = launch_plan(args.gpus, args.dist_backend, os.environ, device_count)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(n, sys.argv[1:]))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world}, --gpus={args.gpus}; using WORLD_SIZE")
+    launch = ("torch.distributed.run child started by bench.py --gpus N" if os.environ.get(SELF_LAUNCH_ENV)
+              else "external launcher (WORLD_SIZE set)" if "WORLD_SIZE" in os.environ else "single process")
 
     import torch
+    if args.dist_backend == "nccl" and local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} has LOCAL_RANK {local}, {torch.cuda.device_count()} GPUs visible")
     if args.dist_backend == "gloo":
         local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
@@ -578,6 +651,16 @@ def main():
     # each batch's u_old moves from its drawn state over the timed steps (the
     # warmup and settle steps leave it unchanged) and is restored after.
     snap = [tuple(a.clone() for a in st_) for st_ in states]
+
+    def marker():
+        """A short kernel on torch's stream with the library's stream idle: a
+        kernel trace is cut between two of them (--markers)."""
+        if args.markers:
+            torch.cuda.synchronize()
+            torch.cuda._sleep(1000)
+            torch.cuda.synchronize()
+
+    marker()
     torch.cuda.synchronize()
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
@@ -587,6 +670,7 @@ def main():
     ctx.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    marker()
     if dist:
         dist.barrier()
     build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
@@ -631,12 +715,14 @@ def main():
     # events on the iterate only (after the headline measurement, untimed for
     # `value`)
     restore(warm=True)
+    marker()
     ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_ITERATE,))
     for i in range(args.steps):
         bind(first + i)
         ctx.step(K, cmpc.CMPC_APPLY_MOVE)
     ctx.synchronize()
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
+    marker()
     ctx.enable_timing(False)
     restore()
     # working-set changes of the timed workload, summed over the K Jacobi
@@ -907,15 +993,18 @@ def main():
             recorded = recorded_run_changes(local)
         except Exception as e:  # reported, never required
             log(f"recorded-run replay failed: {e}")
-    coupled, rc, el_c = None, None, float("inf")
-    if not args.no_coupled and not args.headline_only:
+    def coupled_section(S_local, S_total, note, scaling_note):
+        """SURVEY config 4 on every rank (cmpc.coupled.run_coupled_bench),
+        the max of the elapsed time over ranks; None when any rank failed."""
         from cmpc.coupled import run_coupled_bench
+        rc = None
         try:  # reported beside the metric, never required for it
-            rc = run_coupled_bench(rank, world, local, S_local=8, B=args.coupled_batch, p=args.p, K=K,
-                                   steps=max(5, args.steps // 2), settle_seconds=args.settle_seconds,
-                                   force_collective=bool(dist), tiles=args.coupled_tiles)
+            rc = run_coupled_bench(rank, world, local, S_local=S_local, S_total=S_total, B=args.coupled_batch,
+                                   p=args.p, K=K, steps=max(5, args.steps // 2),
+                                   settle_seconds=args.settle_seconds, force_collective=bool(dist),
+                                   tiles=args.coupled_tiles)
         except Exception as e:
-            log(f"[rank {rank}] coupled section failed: {e}")
+            log(f"[rank {rank}] coupled section (S_total {S_total}) failed: {e}")
         # every rank joins the reduction; a failed rank reports +inf, so the
         # section is dropped everywhere
         tc = torch.tensor([rc["elapsed_s"] if rc else float("inf")], dtype=torch.float64,
@@ -923,27 +1012,46 @@ def main():
         if dist:
             dist.all_reduce(tc, op=dist.ReduceOp.MAX)
         el_c = float(tc.item())
-    if rc and el_c != float("inf"):
-        coupled = dict(rc)
-        coupled.pop("elapsed_s")
-        coupled.update({
+        if not rc or el_c == float("inf"):
+            return None
+        out_c = dict(rc)
+        out_c.pop("elapsed_s")
+        out_c.update({
             "qp_solves_per_s": world * rc["qp_per_gpu"] * K * rc["steps"] / el_c,
             "ms_per_step": el_c / rc["steps"] * 1e3,
             "exchange": ("RCCL all_gather_into_tensor of B x S_local x nV plans per Jacobi iteration"
                          if dist and args.dist_backend == "nccl" else
                          "gloo all_gather of the plans through host memory (rehearsal only)" if dist
                          else "local copy (world size 1)"),
-            "note": "SURVEY config 4: S_total = 8 x world sub-controllers per scenario (synthetic "
-                    "coupling, cmpc/coupled.py), 8 per GPU; step = build + K x (all-gather + "
-                    "coupled iteration), first move applied; with tiles > 1 the scenarios run as "
-                    "that many tiles on their own streams, each tile's all-gather overlapping "
-                    "another tile's iteration (cmpc.coupled.CoupledPipeline; slower at world 1, "
-                    "DESIGN.md section 8); gather_ms (summed over the tiles) from events in a "
-                    "separate pass",
-            "scaling_note": ("not constant work per GPU: S_total = 8 x world, so each QP's f_k update "
-                             "reads nV x (S_total - 1) nV coupling entries and the gathered plans grow "
-                             "with world; a SCALE curve of this section is weak scaling in scenarios "
-                             "per GPU with per-QP work growing linearly in world size")})
+            "note": note, "scaling_note": scaling_note})
+        return out_c
+
+    coupled = coupled_s64 = None
+    if not args.no_coupled and not args.headline_only:
+        common = ("step = build + K x (all-gather + coupled iteration), first move applied; with "
+                  "tiles > 1 the scenarios run as that many tiles on their own streams, each tile's "
+                  "all-gather overlapping another tile's iteration (cmpc.coupled.CoupledPipeline; "
+                  "slower at world 1, DESIGN.md section 8); gather_ms (summed over the tiles) and "
+                  "iterate_kernel_ms (G_ext_hbm_frac: G_ext bytes per iteration / that time / 8 TB/s) "
+                  "from events in separate passes")
+        coupled = coupled_section(
+            8, 8 * world,
+            "SURVEY config 4, 8 sub-controllers per GPU: S_total = 8 x world sub-controllers per "
+            "scenario (synthetic coupling, cmpc/coupled.py); " + common,
+            "not constant work per GPU: S_total = 8 x world, so each QP's f_k update reads nV x "
+            "(S_total - 1) nV coupling entries and the gathered plans grow with world; a SCALE curve "
+            "of this section is weak scaling in scenarios per GPU with per-QP work growing linearly "
+            "in world size (coupled_s64 is the fixed 64-sub-controller system)")
+        # BASELINE config 4's own problem at every world size (VERDICT r5,
+        # next 2): S_total = 64 sub-controllers, 64 / world per GPU, B
+        # scenarios: the same system at world 1, 2, 4 and 8
+        if 64 % world == 0:
+            coupled_s64 = coupled_section(
+                64 // world, 64,
+                "BASELINE config 4's system: S_total = 64 sub-controllers per scenario, S_local = "
+                "64 / world per GPU (all 64 and the whole G_ext on one GPU at world 1); " + common,
+                "strong scaling in sub-controllers: the same 64-sub-controller system of B scenarios "
+                "at every world size, each GPU holding 64 / world of them")
 
     ok_frac = float((st == 0).mean())
     active_frac = float((ws_now != 0).mean())
@@ -964,6 +1072,8 @@ def main():
         "value": value,
         "unit": "QP solves/s",
         "n_gpus": world,
+        "gpus_requested": args.gpus,
+        "launch": launch,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed_max / args.steps * 1e3,
@@ -1042,6 +1152,7 @@ def main():
         "configs": configs,
         "closed_loop_device_resident": closed,
         "coupled": coupled,
+        "coupled_s64": coupled_s64,
     }
     if rank == 0 and world == 1 and not args.no_cpu and not args.headline_only:
         try:

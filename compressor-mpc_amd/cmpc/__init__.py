@@ -302,7 +302,7 @@ class Context:
     def set_build_variant(self, variant: int):
         """CMPC_BUILD_AUTO / CMPC_BUILD_WAVE (one QP per wave) / CMPC_BUILD_ROWS
         (four QPs per wave, one per DPP row) / CMPC_BUILD_SPLIT (one QP per two
-        waves: chain and gather, ny <= 3)."""
+        waves: chain and gather, every ny)."""
         check(self.lib.cmpc_set_build_variant(self._h, int(variant)), "cmpc_set_build_variant")
 
     def last_build_kernel(self) -> int:

@@ -311,12 +311,28 @@ def run_coupled_bench(rank: int, world: int, device: int, S_local: int = 8, B: i
                     c.iterate(k == K - 1)
         torch.cuda.synchronize(device)
         gather_ms = sum(a.elapsed_time(b) for et in ev for a, b in et) / K
+        # the coupled iterate kernel alone (library events on its stream), a
+        # third pass: G_ext's HBM fraction
+        from . import CMPC_KERNEL_ITERATE
+        for c in crs:
+            c.ctx.enable_timing(True, only=(CMPC_KERNEL_ITERATE,))
+        for _ in range(max(1, steps // 2)):
+            cr.step(K)
+        torch.cuda.synchronize(device)
+        it = [c.ctx.kernel_time(CMPC_KERNEL_ITERATE) for c in crs]
+        for c in crs:
+            c.ctx.enable_timing(False)
+        iterate_ms = sum(ms / max(n, 1) for ms, n in it)  # per iteration, summed over the tiles
+        g_bytes = sum(c.G_ext.numel() for c in crs) * 8
         st = np.concatenate([c.ctx.download()[1] for c in crs])
         return {"elapsed_s": elapsed, "steps": steps, "qp_per_gpu": nqp, "S_total": S_total,
                 "S_local": S_local, "B": B, "p": p, "K": K, "tiles": tiles,
-                "G_ext_MB_per_gpu": sum(c.G_ext.numel() for c in crs) * 8 / 1e6,
+                "G_ext_MB_per_gpu": g_bytes / 1e6,
                 "gather_ms_per_iteration": gather_ms,
                 "gather_bytes_per_iteration": world * nqp * cfg.nV * 8,
+                "iterate_kernel_ms": iterate_ms,
+                "G_ext_hbm_GBs": g_bytes / (iterate_ms * 1e-3) / 1e9 if iterate_ms > 0 else None,
+                "G_ext_hbm_frac": g_bytes / (iterate_ms * 1e-3) / 8e12 if iterate_ms > 0 else None,
                 "qp_status_ok_fraction": float((st == 0).mean())}
     finally:
         for c in crs:

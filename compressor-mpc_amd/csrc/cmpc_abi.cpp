@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <chrono>
 #include <vector>
 
@@ -988,7 +989,7 @@ static int control_step(cmpc_ctx* c, const double* u_full, const double* y, int 
     int solver = 0;
     if (cmpc_launch_control_step(C, d.ns, d.ny, d.nu, d.m, c->stream, &solver) == 0) {
       if (check_launch("control step kernel")) return -1;
-      c->last_build = CMPC_BUILD_WAVE;
+      c->last_build = C.b.split ? CMPC_BUILD_SPLIT : CMPC_BUILD_WAVE;
       c->last_solve = solver;
       c->last_step_fused = 1;
       c->obs_steps++;  // the delay-block rings advance by one (cmpc_observe_apply)
@@ -2073,95 +2074,84 @@ int cmpc_qp_solve_batch(int device, int n, int nu, int nqp, const double* H, con
                         const double* lb, const double* ub, const double* lbA, const double* ubA,
                         const uint32_t* ws_in, int max_chg, double* x, int32_t* status,
                         int32_t* nchg, uint32_t* ws_out, uint8_t* trace, int32_t* ntrace) {
-  if (nqp <= 0) return 0;
-  HIP_TRY(hipSetDevice(device));
-  const size_t q = (size_t)nqp;
-  double* dH; double* dg; double* dlb; double* dub; double* dlbA; double* dubA; double* dx;
-  uint32_t *dws, *dwo; int32_t *dst, *dnc, *dnt; uint8_t* dtr;
-  HIP_TRY(hipMalloc(&dH, sizeof(double) * q * n * n));
-  HIP_TRY(hipMalloc(&dg, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dlb, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dub, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dlbA, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dubA, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dx, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dws, sizeof(uint32_t) * q));
-  HIP_TRY(hipMalloc(&dwo, sizeof(uint32_t) * q));
-  HIP_TRY(hipMalloc(&dst, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dnc, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dnt, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dtr, 16 * q));
-  HIP_TRY(hipMemcpy(dH, H, sizeof(double) * q * n * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dg, g, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dlb, lb, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dub, ub, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dlbA, lbA, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dubA, ubA, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dws, ws_in, sizeof(uint32_t) * q, hipMemcpyHostToDevice));
-  QpBatchParams P{dH, dg, dlb, dub, dlbA, dubA, dws, dx, dst, dnc, dnt, dwo, dtr, nqp, max_chg};
-  if (cmpc_launch_qp_batch(P, n, nu, nullptr)) return fail("qp batch kernel not instantiated");
-  if (check_launch("qp batch kernel")) return -1;
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(x, dx, sizeof(double) * q * n, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(nchg, dnc, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(ws_out, dwo, sizeof(uint32_t) * q, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(trace, dtr, 16 * q, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(ntrace, dnt, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
-  void* bufs[] = {dH, dg, dlb, dub, dlbA, dubA, dx, dws, dwo, dst, dnc, dnt, dtr};
-  for (void* b : bufs) (void)hipFree(b);
-  return 0;
+  return cmpc_qp_solve_batch_map(device, n, nu, 0, nqp, H, g, nullptr, nullptr, lb, ub, lbA, ubA, ws_in, max_chg, x,
+                                 status, nchg, ws_out, trace, ntrace);
 }
 
+// cmpc_qp_solve_batch(_map): host arrays in, host arrays out.  The dimensions
+// are checked against the kernel instances before anything is allocated, the
+// device buffers are released on every exit path, and only the stream of the
+// launch is waited for.
 int cmpc_qp_solve_batch_map(int device, int n, int nu, int nvo, int nqp, const double* H, const double* f,
                             const double* G, const double* d, const double* lb, const double* ub,
                             const double* lbA, const double* ubA, const uint32_t* ws_in, int max_chg, double* x,
                             int32_t* status, int32_t* nchg, uint32_t* ws_out, uint8_t* trace, int32_t* ntrace) {
-  if (nvo == 0)
-    return cmpc_qp_solve_batch(device, n, nu, nqp, H, f, lb, ub, lbA, ubA, ws_in, max_chg, x, status, nchg, ws_out,
-                               trace, ntrace);
+  if (nvo < 0) return fail("cmpc_qp_solve_batch_map: nvo < 0");
+  if (nvo > 0 && (!G || !d)) return fail("cmpc_qp_solve_batch_map: G and d required for nvo > 0");
+  if (nvo > 0 ? !cmpc_qp_batch_map_supported(n, nu, nvo) : !cmpc_qp_batch_supported(n, nu))
+    return fail(nvo > 0 ? "map-form qp batch kernel not instantiated for (n, nu, nvo) = (" + std::to_string(n) +
+                              ", " + std::to_string(nu) + ", " + std::to_string(nvo) + ")"
+                        : "qp batch kernel not instantiated for (n, nu) = (" + std::to_string(n) + ", " +
+                              std::to_string(nu) + ")");
   if (nqp <= 0) return 0;
-  if (nvo < 0 || !G || !d) return fail("cmpc_qp_solve_batch_map: G and d required for nvo > 0");
   HIP_TRY(hipSetDevice(device));
   const size_t q = (size_t)nqp;
-  double* dH; double* dg; double* dG; double* dd; double* dlb; double* dub; double* dlbA; double* dubA; double* dx;
-  uint32_t *dws, *dwo; int32_t *dst, *dnc, *dnt; uint8_t* dtr;
-  HIP_TRY(hipMalloc(&dH, sizeof(double) * q * n * n));
-  HIP_TRY(hipMalloc(&dg, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dG, sizeof(double) * q * n * nvo));
-  HIP_TRY(hipMalloc(&dd, sizeof(double) * q * nvo));
-  HIP_TRY(hipMalloc(&dlb, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dub, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dlbA, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dubA, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dx, sizeof(double) * q * n));
-  HIP_TRY(hipMalloc(&dws, sizeof(uint32_t) * q));
-  HIP_TRY(hipMalloc(&dwo, sizeof(uint32_t) * q));
-  HIP_TRY(hipMalloc(&dst, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dnc, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dnt, sizeof(int32_t) * q));
-  HIP_TRY(hipMalloc(&dtr, 16 * q));
+  struct Bufs {  // scope guard: every buffer allocated below is freed on return
+    std::vector<void*> p;
+    ~Bufs() {
+      for (void* b : p) (void)hipFree(b);
+    }
+  } bufs;
+  auto alloc = [&](auto** ptr, size_t bytes) -> hipError_t {
+    void* v = nullptr;
+    const hipError_t e = hipMalloc(&v, bytes ? bytes : 8);
+    if (e == hipSuccess) bufs.p.push_back(v);
+    *ptr = static_cast<std::remove_pointer_t<decltype(ptr)>>(v);
+    return e;
+  };
+  double *dH, *dg, *dG = nullptr, *dd = nullptr, *dlb, *dub, *dlbA, *dubA, *dx;
+  uint32_t *dws, *dwo;
+  int32_t *dst, *dnc, *dnt;
+  uint8_t* dtr;
+  HIP_TRY(alloc(&dH, sizeof(double) * q * n * n));
+  HIP_TRY(alloc(&dg, sizeof(double) * q * n));
+  if (nvo > 0) {
+    HIP_TRY(alloc(&dG, sizeof(double) * q * n * nvo));
+    HIP_TRY(alloc(&dd, sizeof(double) * q * nvo));
+  }
+  HIP_TRY(alloc(&dlb, sizeof(double) * q * n));
+  HIP_TRY(alloc(&dub, sizeof(double) * q * n));
+  HIP_TRY(alloc(&dlbA, sizeof(double) * q * n));
+  HIP_TRY(alloc(&dubA, sizeof(double) * q * n));
+  HIP_TRY(alloc(&dx, sizeof(double) * q * n));
+  HIP_TRY(alloc(&dws, sizeof(uint32_t) * q));
+  HIP_TRY(alloc(&dwo, sizeof(uint32_t) * q));
+  HIP_TRY(alloc(&dst, sizeof(int32_t) * q));
+  HIP_TRY(alloc(&dnc, sizeof(int32_t) * q));
+  HIP_TRY(alloc(&dnt, sizeof(int32_t) * q));
+  HIP_TRY(alloc(&dtr, 16 * q));
   HIP_TRY(hipMemcpy(dH, H, sizeof(double) * q * n * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dg, f, sizeof(double) * q * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dG, G, sizeof(double) * q * n * nvo, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dd, d, sizeof(double) * q * nvo, hipMemcpyHostToDevice));
+  if (nvo > 0) {
+    HIP_TRY(hipMemcpy(dG, G, sizeof(double) * q * n * nvo, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dd, d, sizeof(double) * q * nvo, hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy(dlb, lb, sizeof(double) * q * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dub, ub, sizeof(double) * q * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dlbA, lbA, sizeof(double) * q * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dubA, ubA, sizeof(double) * q * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dws, ws_in, sizeof(uint32_t) * q, hipMemcpyHostToDevice));
   QpBatchParams P{dH, dg, dlb, dub, dlbA, dubA, dws, dx, dst, dnc, dnt, dwo, dtr, nqp, max_chg, dG, dd, nvo};
-  if (cmpc_launch_qp_batch_map(P, n, nu, nvo, nullptr)) return fail("map-form qp batch kernel not instantiated");
-  if (check_launch("map-form qp batch kernel")) return -1;
-  HIP_TRY(hipDeviceSynchronize());
+  const int lr = nvo > 0 ? cmpc_launch_qp_batch_map(P, n, nu, nvo, nullptr) : cmpc_launch_qp_batch(P, n, nu, nullptr);
+  if (lr) return fail("qp batch kernel not instantiated");
+  if (check_launch("qp batch kernel")) return -1;
+  HIP_TRY(hipStreamSynchronize(nullptr));
   HIP_TRY(hipMemcpy(x, dx, sizeof(double) * q * n, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(status, dst, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(nchg, dnc, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ws_out, dwo, sizeof(uint32_t) * q, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(trace, dtr, 16 * q, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ntrace, dnt, sizeof(int32_t) * q, hipMemcpyDeviceToHost));
-  void* bufs[] = {dH, dg, dG, dd, dlb, dub, dlbA, dubA, dx, dws, dwo, dst, dnc, dnt, dtr};
-  for (void* b : bufs) (void)hipFree(b);
   return 0;
 }
 

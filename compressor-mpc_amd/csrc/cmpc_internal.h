@@ -313,6 +313,9 @@ int cmpc_launch_solve(const SolveParams& P, int nV, int nu, int nVo,
 int cmpc_launch_solve_rows(const SolveParams& P, int nV, int nu, int nVo, void* stream);
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream);
 int cmpc_launch_qp_batch_map(const QpBatchParams& P, int n, int nu, int nvo, void* stream);
+// the (n, nu[, nvo]) the two launchers above have instances for
+bool cmpc_qp_batch_supported(int n, int nu);
+bool cmpc_qp_batch_map_supported(int n, int nu, int nvo);
 // Plant simulation (sim.hip)
 struct SimParams {
   double* x;              // B * ns

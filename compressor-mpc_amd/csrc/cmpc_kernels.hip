@@ -1213,6 +1213,12 @@ int cmpc_launch_qp_batch_map(const QpBatchParams& P, int n, int nu, int nvo, voi
   return -1;
 }
 
+bool cmpc_qp_batch_map_supported(int n, int nu, int nvo) {
+  return (n == 4 && nu == 2 && nvo == 4) || (n == 6 && nu == 2 && nvo == 6) || (n == 2 && nu == 2 && nvo == 2);
+}
+
+bool cmpc_qp_batch_supported(int n, int nu) { return (n == 4 && nu == 2) || (n == 8 && nu == 4); }
+
 int cmpc_launch_qp_batch(const QpBatchParams& P, int n, int nu, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int grid = (P.nqp + CMPC_SOLVE_THREADS - 1) / CMPC_SOLVE_THREADS;

@@ -165,16 +165,19 @@ int cmpc_build(cmpc_ctx* ctx);
  * CMPC_BUILD_ROWS four QPs per wave, one per 16-lane DPP row (m <= 2, LDS
  * fits); CMPC_BUILD_WAVE one QP per wave (every instantiated dimension set);
  * CMPC_BUILD_SPLIT one QP per two waves, the DPP chain in one and the gather
- * in the other (ny <= 3); CMPC_BUILD_AUTO (default) rows where its LDS fits
- * and the batch fills the SIMDs, else split up to one QP per SIMD (ny <= 3),
- * else wave.  All give the same QP bit for bit. */
+ * in the other (every ny, the ny = 4 simulation pre-pass included);
+ * CMPC_BUILD_AUTO (default) rows where its LDS fits and the batch fills the
+ * SIMDs, else split up to one QP per SIMD, else wave.  WAVE and SPLIT give
+ * the same QP bit for bit; ROWS sums in another order (agreement within
+ * rounding, 1e-11 relative). */
 #define CMPC_BUILD_AUTO 0
 #define CMPC_BUILD_WAVE 1
 #define CMPC_BUILD_ROWS 2
 #define CMPC_BUILD_SPLIT 3
 int cmpc_set_build_variant(cmpc_ctx* ctx, int variant);
-/* The build kernel the last cmpc_build launched (CMPC_BUILD_WAVE or
- * CMPC_BUILD_ROWS), 0 before the first build, <0 on a null context. */
+/* The build kernel the last cmpc_build, cmpc_step or cmpc_control_step
+ * launched (CMPC_BUILD_WAVE, CMPC_BUILD_ROWS or CMPC_BUILD_SPLIT), 0 before the
+ * first build, <0 on a null context. */
 int cmpc_last_build_kernel(cmpc_ctx* ctx);
 /* Solve-kernel selection for cmpc_iterate / cmpc_init_warmstart /
  * cmpc_get_input (the same results bit for bit):

@@ -479,6 +479,10 @@ class DistributedSolver : public MpcQpSolver {
       *du_out = SolveQP(*qp, u_old);
       return;
     }
+    // the sizes Solve checks, before ApplyOtherInput writes f and SolveMap
+    // reads H, f and G into host copies of nV x nV, nV and nV x nVo doubles
+    if (static_cast<int>(qp->H.size()) != nV * nV || static_cast<int>(qp->f.size()) != nV)
+      throw Error("UpdateAndSolveQP: QP of the wrong size");
     if (static_cast<int>(qp->G.size()) != nV * nVo) throw Error("UpdateAndSolveQP: QP without G");
     const std::vector<double> f0 = qp->f;  // the step's f
     const std::vector<double> d = OtherPlans(du_other);

@@ -163,6 +163,24 @@ int main(int argc, char** argv) {
           else ds[s].UpdateAndSolveQP(&copy, &du_ds, uo_s[s].data(), du_last.data());
           solver_equal = solver_equal && ds[s].last_status() == status[s] &&
                          std::equal(du_ds.begin(), du_ds.end(), du_new.begin() + s * nV);
+          if (k == 0 && i == 0 && !du_last.empty()) {
+            // a mis-sized QP is an Error, not an out-of-bounds host access
+            // (Solve's size check, repeated before ApplyOtherInput)
+            bool refused = true;
+            for (int bad = 0; bad < 2; ++bad) {
+              QP wrong = qps[s];
+              if (bad == 0) wrong.H.pop_back();
+              else wrong.f.pop_back();
+              std::vector<double> du_w;
+              try {
+                ds[s].UpdateAndSolveQP(&wrong, &du_w, uo_s[s].data(), du_last.data());
+                refused = false;
+              } catch (const Error&) {
+              }
+            }
+            std::printf("mis-sized QP: %s\n", refused ? "refused" : "ACCEPTED");
+            solver_equal = solver_equal && refused;
+          }
         }
         du_prev = du_new;
       }

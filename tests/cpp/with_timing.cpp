@@ -151,6 +151,18 @@ int main(int argc, char** argv) {
       mean_ns += recs[k].ns;
     }
     std::fclose(f);
+    // the same u and y at full precision (%.17g), one record per line, beside
+    // the %g file: the tests tell a rounding-boundary tie of the printed
+    // sixth digit from a real difference (tests/golden_cases.py)
+    FILE* ff = std::fopen((path + ".full").c_str(), "w");
+    if (!ff) throw Error("cannot write " + path + ".full");
+    for (const Record& r : recs) {
+      for (double v : r.u) std::fprintf(ff, "%.17g ", v);
+      std::fprintf(ff, "|");
+      for (double v : r.y) std::fprintf(ff, " %.17g", v);
+      std::fprintf(ff, "\n");
+    }
+    std::fclose(ff);
     std::printf("{\"records\": %zu, \"file\": \"%s\", \"mean_step_us\": %.2f}\n", recs.size(), path.c_str(),
                 recs.empty() ? 0.0 : mean_ns / recs.size() * 1e-3);
     return 0;

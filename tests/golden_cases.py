@@ -91,19 +91,30 @@ def six_digit_rows(got, ref, boundary_rel=1e-9):
     return np.array(sorted(bad), dtype=int), np.array(sorted(tie), dtype=int)
 
 
-def six_digit_strings_ok(printed, ref):
+def six_digit_strings_ok(printed, ref, full=None, boundary_rel=1e-9):
     """A printed record (strings, %g) against the reference's: equal to 6
-    digits, or one unit of the 6th digit apart (a rounding-boundary tie, see
-    six_digit_rows; the printed text cannot tell which).  Returns
-    (equal, tie)."""
+    digits, or a rounding-boundary tie.  The printed text cannot tell a tie
+    from a real last-digit difference, so a tie needs the full-precision
+    values `full` the harness wrote beside it (with_timing's .full file): each
+    differing value must lie within boundary_rel of a %.6g rounding boundary
+    and one unit of the 6th digit from the reference, the rule of
+    six_digit_rows.  Without `full` no tie is accepted.  Returns (equal, tie)."""
     a = [_six(float(v)) for v in printed]
     b = [_six(float(v)) for v in ref]
     if a == b:
         return True, False
-    for x, y in zip(a, b):
-        if x != y:
-            m = max(abs(x), abs(y))
-            unit = 10.0 ** (np.floor(np.log10(m)) - 5) if m > 0 else 0.0
-            if abs(x - y) > 1.01 * unit:
-                return False, False
-    return False, True
+    if full is None or len(full) != len(a):
+        return False, False
+    if [_six(float(v)) for v in full] != a:
+        return False, False  # the .full values are not the printed record's
+    bad, tie = six_digit_rows([list(map(float, full))], [list(map(float, ref))], boundary_rel)
+    return False, bool(len(tie)) and not len(bad)
+
+
+def read_full(path):
+    """with_timing's .full sidecar: per record the u and y values at %.17g."""
+    out = []
+    for ln in open(path).read().splitlines():
+        u, y = ln.split("|")
+        out.append(([float(v) for v in u.split()], [float(v) for v in y.split()]))
+    return out

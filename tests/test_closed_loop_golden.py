@@ -198,6 +198,14 @@ def test_six_digit_rows_tie_rule():
     ref = np.array([[-8.99513e-08, 1.0], [1.23457e-3, 2.0], [1.2346e-3, 0.5]])
     bad, tie = GC.six_digit_rows(got, ref)
     assert list(tie) == [1] and list(bad) == [2]  # (row 0 prints equal)
-    assert GC.six_digit_strings_ok(["1.23456"], [1.23457]) == (False, True)
-    assert GC.six_digit_strings_ok(["1.23456"], [1.23458]) == (False, False)
+    # a printed tie needs the full-precision value at a rounding boundary
+    # (the %g text alone cannot tell a tie from a drift)
+    at = np.nextafter(1.234565, 0.0)  # prints 1.23456, within 1e-9 of the boundary
+    assert "%.6g" % at == "1.23456"
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457], [at]) == (False, True)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457]) == (False, False)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457], [1.23456]) == (False, False)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457], [1.2345649]) == (False, False)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23458], [at]) == (False, False)
+    assert GC.six_digit_strings_ok(["1.23456"], [1.23457], [1.23458]) == (False, False)  # not the printed value
     assert GC.six_digit_strings_ok(["0", "2.5"], [1e-13, 2.5]) == (True, False)

@@ -150,11 +150,13 @@ def test_gpu_cpp_harness_writes_reference_run(name, tmp_path):
     ur, yr = gold[f"{plant}_{key}_u"], gold[f"{plant}_{key}_y"]
     assert len(recs) == len(ur) == 10000
     first = json.load(open(os.path.join(HERE, "golden", f"traj_{plant}_{key}.json")))["records"]
+    full = GC.read_full(str(tmp_path / "parallel" / "out.dat") + ".full")
+    assert len(full) == len(recs)
     ties = 0
     for k, rec in enumerate(recs):
         assert float(rec["t"]) == float("%g" % (k * 0.05)), (k, rec["t"])
-        for key_, ref in (("u", ur[k]), ("y", yr[k])):
-            eq, tie = GC.six_digit_strings_ok(rec[key_].split(), ref)
+        for i, (key_, ref) in enumerate((("u", ur[k]), ("y", yr[k]))):
+            eq, tie = GC.six_digit_strings_ok(rec[key_].split(), ref, full[k][i])
             assert eq or tie, (k, key_, rec[key_], ref)
             ties += tie
         if k < len(first):
@@ -181,9 +183,10 @@ def test_gpu_cpp_harness_timed_prefix_keeps_trajectory(n_timing, tmp_path):
     gold = np.load(os.path.join(HERE, "golden", "traj_long.npz"))
     ur = gold["par_coop9_u"]
     assert len(recs) == 1200
+    full = GC.read_full(str(tmp_path / "parallel" / "out.dat") + ".full")
     ties = 0
     for k, rec in enumerate(recs):
-        eq, tie = GC.six_digit_strings_ok(rec["u"].split(), ur[k])
+        eq, tie = GC.six_digit_strings_ok(rec["u"].split(), ur[k], full[k][0])
         assert eq or tie, (k, rec["u"], ur[k])
         ties += tie
     assert ties <= 2, ties
@@ -224,6 +227,10 @@ def test_gpu_distributed_controller_api_matches_nerve_center(name, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("step ")]
     assert len(lines) == 6 and all(" equal " in l for l in lines), r.stdout
+    # UpdateAndSolveQP refuses a mis-sized QP wherever it is called
+    assert "ACCEPTED" not in r.stdout
+    if ctype != "cent":
+        assert "mis-sized QP: refused" in r.stdout, r.stdout
     # steps 1, 3, 5 ran through the timed overloads (UpdateU / GenerateInitialQP
     # / GetInput on a CpuTimer, distributed_controller.h:155-183): the same
     # bits, and the timers accumulated

@@ -1,0 +1,60 @@
+"""Kernel statistics of the headline's own launches, cut from a rocprofv3
+kernel trace of `bench.py --headline-only --markers`.
+
+The bench brackets two passes with torch.cuda._sleep marker launches:
+  pass 1: the timed steps (build with events, the iterate without),
+  pass 2: the same step loop again with events on the iterate only.
+The build's rocprof average over pass 1 is compared with the bench line's
+roofline.avg_launch_ms, the iterate's over pass 2 with
+kernels_ms_per_step.iterate (the profiled run's own events, or those of an
+unprofiled reference line when given).
+usage: python tools/headline_pass_stats.py <kernel_trace.csv> <profiled bench json>
+       [<reference bench json>] [out.csv]"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+
+
+def last_line(path):
+    return [json.loads(x) for x in open(path).read().splitlines() if x.strip().startswith("{")][-1]
+
+
+def main():
+    trace, bench = sys.argv[1], sys.argv[2]
+    ref = last_line(sys.argv[3] if len(sys.argv) > 3 else bench)
+    out = sys.argv[4] if len(sys.argv) > 4 else None
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "spin" in r["Kernel_Name"] or "sleep" in r["Kernel_Name"]]
+    if len(marks) != 4:
+        sys.exit(f"expected 4 marker launches, found {len(marks)}")
+    ev = {"build": ref["roofline"]["avg_launch_ms"] * 1e3,
+          "iterate": ref["kernels_ms_per_step"]["iterate"] * 1e3}
+    table = []
+    for n, (pname, role_of_pass) in enumerate((("timed_steps", "build"), ("iterate_event_pass", "iterate"))):
+        a, b = marks[2 * n], marks[2 * n + 1]
+        dur = defaultdict(list)
+        for r in rows[a + 1:b]:
+            dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for name, d in dur.items():
+            role = "build" if "build" in name else "iterate" if "solve" in name else None
+            avg = sum(d) / len(d)
+            e = ev.get(role) if role == role_of_pass else None
+            table.append({"pass": pname, "kernel": name, "calls": len(d), "rocprof_avg_us": round(avg, 3),
+                          "bench_event_us": round(e, 3) if e else None,
+                          "ratio": round(avg / e, 4) if e else None})
+    for t in table:
+        print(t)
+    if out:
+        with open(out, "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(table[0]))
+            w.writeheader()
+            w.writerows(table)
+
+
+if __name__ == "__main__":
+    main()
