@@ -80,6 +80,9 @@
 #ifndef CMPC_ROWS_SPLIT
 #define CMPC_ROWS_SPLIT 5  // chain link groups before the gather columns' running sums (0: none)
 #endif
+#ifndef CMPC_ROWS_ZL
+#define CMPC_ROWS_ZL 1  // the P chain's accumulators zeroed by LDS reads (the parallel plant's kernels)
+#endif
 #ifndef CMPC_ROWS_PRIO
 #define CMPC_ROWS_PRIO 1  // 1: priority by progress; 2: + prologue at top priority
 #endif
@@ -134,6 +137,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   // horizons: bit-identical, ser-coop p = 100 -1.2 %, par-cent p = 200
   // -0.5 %, profiles/r3_pipe_wpe2_ab.txt)
   constexpr bool PIPE = CMPC_ROWS_SPLIT > 0 && CMPC_ROWS_AS0 && ((NY <= 3 && NV <= 4 && !RING) || WPE <= 2);
+  constexpr bool ZL = CMPC_ROWS_ZL && PIPE && NY <= 3 && NV <= 4 && !RING && FUSE == 0;
   static_assert(NG <= 16 && NS + NUT <= 16 && NS + NY + ND <= 16, "lane budget");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -289,13 +293,29 @@ void cmpc_build_rows_kernel(BuildParams P) {
     if (CMPC_PX != 1) {
       const int nq = min(4, nqp - 4 * g);
       const int nchunk = nq * rec_len / 2;
-      const double* gsrc = P.lin + (size_t)4 * g * rec_len;
-      for (int c0 = 0; c0 < nchunk; c0 += 64) {
-        if (c0 + lane < nchunk)
-          __builtin_amdgcn_global_load_lds(
-              (__attribute__((address_space(1))) void*)(gsrc + 2 * (c0 + lane)),
-              (__attribute__((address_space(3))) void*)(wreg + 2 * c0), 16, 0, 0);
+      // Whole 64-lane chunks in blocks of four sharing one global address
+      // and one LDS base (M0): the instruction offset advances both by the
+      // chunk's 1 KiB (offset field < 4 KiB), so a block costs one 64-bit
+      // address add instead of an address, a readfirstlane and an exec mask
+      // per chunk; the partial chunk last, lane-masked.
+      const int nfull = nchunk >> 6;
+      const double* gsrc = P.lin + (size_t)4 * g * rec_len + 2 * lane;
+      int c = 0;
+      for (; c + 4 <= nfull; c += 4) {
+        auto* gp = (__attribute__((address_space(1))) void*)(gsrc + 128 * c);
+        auto* lp = (__attribute__((address_space(3))) void*)(wreg + 128 * c);
+        __builtin_amdgcn_global_load_lds(gp, lp, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(gp, lp, 16, 1024, 0);
+        __builtin_amdgcn_global_load_lds(gp, lp, 16, 2048, 0);
+        __builtin_amdgcn_global_load_lds(gp, lp, 16, 3072, 0);
       }
+      for (; c < nfull; ++c)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(gsrc + 128 * c),
+                                         (__attribute__((address_space(3))) void*)(wreg + 128 * c), 16, 0, 0);
+      if (lane < (nchunk & 63))
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(gsrc + 128 * nfull),
+                                         (__attribute__((address_space(3))) void*)(wreg + 128 * nfull), 16, 0,
+                                         0);
     }
     double uo[NDW];
 #pragma unroll
@@ -362,7 +382,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
       double t = 0.0;
 #pragma unroll
       for (int o2 = 0; o2 < NY; ++o2)
-        if (o2 >= o) t += lwt[o * NY + o2] * cs[o2];
+        if (o2 >= o) t = __builtin_fma(lwt[o * NY + o2], cs[o2], t);  // one VALU per term
       if (j < nobs) chq[o * 16 + j] = t;
       pP[o] = st ? t : 0.0;  // P_0 = C_hat[:, :ns]
     }
@@ -376,8 +396,10 @@ void cmpc_build_rows_kernel(BuildParams P) {
         const int t = j + 16 * i;
         if (t < WL) wk[t] = (t < dlen[k]) ? xw[k][i] - uo[k] : 0.0;
       }
-      const double* gxa = P.lin + (size_t)qq * rec_len + P.off_x;  // long horizons only
-      for (int t = j + 64; t < WL; t += 16) wk[t] = (t < dlen[k]) ? gxa[boff[k] + t - 1] - uo[k] : 0.0;
+      if (WL > 64) {  // long horizons only (a uniform branch: no per-lane loop set-up)
+        const double* gxa = P.lin + (size_t)qq * rec_len + P.off_x;
+        for (int t = j + 64; t < WL; t += 16) wk[t] = (t < dlen[k]) ? gxa[boff[k] + t - 1] - uo[k] : 0.0;
+      }
     }
     // simulation chain initialisation
     double base = 0.0, pS = 0.0, yh = 0.0;
@@ -387,7 +409,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
       base = fj;
       pS = base;
 #pragma unroll
-      for (int k = 0; k < ND; ++k) pS += mS[NS + k] * wtab[(R * ND + k) * WL];  // x_1 = f + Adelay w_0
+      for (int k = 0; k < ND; ++k) pS = __builtin_fma(mS[NS + k], wtab[(R * ND + k) * WL], pS);  // x_1 = f + Adelay w_0
     } else if (ol) {
 #pragma unroll
       for (int l = 0; l < NS; ++l) mS[l] = chq[oo * 16 + l];
@@ -395,10 +417,10 @@ void cmpc_build_rows_kernel(BuildParams P) {
       double t = 0.0;
 #pragma unroll
       for (int d = 0; d < KX; ++d)
-        if (d < ndist) t += chq[oo * 16 + NS + d] * kx[d];
+        if (d < ndist) t = __builtin_fma(chq[oo * 16 + NS + d], kx[d], t);
 #pragma unroll
       for (int o2 = 0; o2 < NY; ++o2)
-        if (o2 >= oo) t += lwt[oo * NY + o2] * ky[o2];
+        if (o2 >= oo) t = __builtin_fma(lwt[oo * NY + o2], ky[o2], t);
       base = t;
       const double* yl = ylT + (s * NY + oo) * yls;
       yh = yl[0];
@@ -489,15 +511,22 @@ void cmpc_build_rows_kernel(BuildParams P) {
 #define CMPC_ROWS_AS_BEGIN() double aS = PIPE ? aS0 : base + yh;
 #define CMPC_ROWS_AS_END() \
   if constexpr (PIPE) aS0 = base + yh;
+// ZL: the P chain's accumulators start from zeros read from LDS (issued at
+// the end of the previous step) instead of a v_mov_b64 each: CDNA4 has no
+// non-accumulating FP64 DPP multiply, so every step needs NY zeroed
+// accumulators, and the LDS pipe has the issue slots the VALU lacks
 #define CMPC_ROWS_STEP(u)                                                   \
   {                                                                         \
     CMPC_ROWS_AS_BEGIN()                                                    \
     yh = yp[u];                                                             \
     double aP[NY];                                                          \
-    _Pragma("unroll") for (int o = 0; o < NY; ++o) aP[o] = 0.0;             \
+    _Pragma("unroll") for (int o = 0; o < NY; ++o) aP[o] = ZL ? zn[o] : 0.0; \
     CMPC_ROWS_CG()                                                          \
     _Pragma("unroll") for (int o = 0; o < NY; ++o) pP[o] = aP[o];           \
     pS = aS;                                                                \
+    if constexpr (ZL) {                                                     \
+      _Pragma("unroll") for (int o = 0; o < NY; ++o) zn[o] = zeros[o];      \
+    }                                                                       \
     if (CMPC_RX != 1 && CMPC_RX != 4) {                                     \
       _Pragma("unroll") for (int o = 0; o < NY; ++o) wq[(u) * NY + o] = aP[o]; \
       zq[(u) * NY] = aS;                                                    \
@@ -526,6 +555,9 @@ void cmpc_build_rows_kernel(BuildParams P) {
     int r = 0;
     double aS0 = base + yh;  // CMPC_ROWS_AS0: start value of the next step's free-response chain
     (void)aS0;
+    double zn[NY];  // ZL: the next step's zeroed P accumulators
+#pragma unroll
+    for (int o = 0; o < NY; ++o) zn[o] = ZL ? zeros[o] : 0.0;
     for (int sg = 0; sg <= nseg; ++sg) {
       int r_end = pp;
 #pragma unroll
