@@ -533,6 +533,11 @@ def main():
                     help="a torch.cuda._sleep launch before and after the timed steps and before and "
                          "after the iterate's event pass, so that a kernel trace of the run can be cut "
                          "to exactly those launches (tools/headline_pass_stats.py)")
+    ap.add_argument("--build-events", choices=("timed", "separate"), default="timed",
+                    help="timed: the build's HIP events ride on the timed steps (the roofline's "
+                         "launch time is the timed launches'); separate: the timed steps run without "
+                         "events and the build's launch time comes from a second pass of the same "
+                         "steps (A/B of the events' own cost)")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--configs-only", action="store_true",
                     help="only the SURVEY-config section's GPU configs (2, 3, 5), one JSON line: "
@@ -662,7 +667,7 @@ def main():
 
     marker()
     torch.cuda.synchronize()
-    ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+    ctx.enable_timing(args.build_events == "timed", only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
     for i in range(args.steps):
         bind(first + i)
@@ -674,7 +679,7 @@ def main():
     if dist:
         dist.barrier()
     build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
-    if n_build == 0:
+    if n_build == 0 and args.build_events == "timed":
         # the steps ran fused (a small --batch, CMPC_STEP_AUTO): the build
         # kernel's own launch time from a build-only pass for the roofline
         ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
@@ -723,6 +728,15 @@ def main():
     ctx.synchronize()
     iter_ms, n_iter = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
     marker()
+    if args.build_events == "separate":
+        # the build's launch time from a second pass of the timed steps
+        restore(warm=True)
+        ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+        for i in range(args.steps):
+            bind(first + i)
+            ctx.step(K, cmpc.CMPC_APPLY_MOVE)
+        ctx.synchronize()
+        build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
     ctx.enable_timing(False)
     restore()
     # working-set changes of the timed workload, summed over the K Jacobi
@@ -1128,7 +1142,9 @@ def main():
         },
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1),
-                                "note": "build: HIP events on every timed step; iterate: events in "
+                                "build_events": args.build_events,
+                                "note": "build: HIP events on every timed step (--build-events timed) or "
+                                        "in a later pass of the same steps (separate); iterate: events in "
                                         "a second pass of the same step loop after the timed steps"},
         "k1": k1,
         "qp_status_ok_fraction": ok_frac,

@@ -4,8 +4,8 @@ kernel trace of `bench.py --headline-only --markers`.
 The bench brackets two passes with torch.cuda._sleep marker launches:
   pass 1: the timed steps (build with events, the iterate without),
   pass 2: the same step loop again with events on the iterate only.
-The build's rocprof average over pass 1 is compared with the bench line's
-roofline.avg_launch_ms, the iterate's over pass 2 with
+The build's rocprof averages over both passes are compared with the bench
+line's roofline.avg_launch_ms, the iterate's over pass 2 with
 kernels_ms_per_step.iterate (the profiled run's own events, or those of an
 unprofiled reference line when given).
 usage: python tools/headline_pass_stats.py <kernel_trace.csv> <profiled bench json>
@@ -43,7 +43,9 @@ def main():
         for name, d in dur.items():
             role = "build" if "build" in name else "iterate" if "solve" in name else None
             avg = sum(d) / len(d)
-            e = ev.get(role) if role == role_of_pass else None
+            # the build runs in both passes (the iterate pass replays the same
+            # steps): both are compared with the build's events
+            e = ev.get(role) if (role == role_of_pass or role == "build") else None
             table.append({"pass": pname, "kernel": name, "calls": len(d), "rocprof_avg_us": round(avg, 3),
                           "bench_event_us": round(e, 3) if e else None,
                           "ratio": round(avg / e, 4) if e else None})
