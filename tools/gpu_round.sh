@@ -10,7 +10,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 900 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --headline-only --markers > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu --headline-only --markers > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit $?
 # the headline's timed steps and iterate pass cut from that trace (markers)
 python3 tools/headline_pass_stats.py gpurun_out/prof_$TAG/run_kernel_trace.csv gpurun_out/benchprof_$TAG.json gpurun_out/bench_$TAG.json gpurun_out/headline_pass_$TAG.csv > gpurun_out/headline_pass_$TAG.txt 2>&1
 # the SURVEY configs' own kernels (no headline launches in this trace): their
