@@ -253,6 +253,13 @@ def test_gpu_bench_force_dist_single_rank():
     assert d["qp_status_ok_fraction"] == 1.0
     assert d["coupled"]["exchange"].startswith("RCCL")
     assert d["coupled"]["qp_status_ok_fraction"] == 1.0
+    # config 4's own 64-sub-controller system: all 64 on
+    # this one rank, its coupling matrix's HBM fraction from the iterate events
+    c64 = d["coupled_s64"]
+    assert c64["S_total"] == 64 and c64["S_local"] == 64 and c64["qp_per_gpu"] == 64 * 512
+    assert c64["qp_status_ok_fraction"] == 1.0
+    assert 0.0 < c64["G_ext_hbm_frac"] < 1.0
+    assert d["n_gpus"] == d["gpus_requested"] == 1
     # the recorded run's solver load beside the synthetic one
     assert d["recorded_run_working_set_changes_per_qp_step"] == d["recorded_run"]["working_set_changes_per_qp_step"]
     assert d["recorded_run_working_set_changes_per_qp_step"] < d["working_set_changes_per_qp_step"]
