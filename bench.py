@@ -538,6 +538,9 @@ def main():
                          "launch time is the timed launches'); separate: the timed steps run without "
                          "events and the build's launch time comes from a second pass of the same "
                          "steps (A/B of the events' own cost)")
+    ap.add_argument("--build-event-stride", type=int, default=1,
+                    help="with --build-events timed: event-stamp every n-th timed build launch only "
+                         "(cmpc_set_timing_stride; the roofline's launch time is the mean of those)")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--configs-only", action="store_true",
                     help="only the SURVEY-config section's GPU configs (2, 3, 5), one JSON line: "
@@ -667,6 +670,7 @@ def main():
 
     marker()
     torch.cuda.synchronize()
+    ctx.set_timing_stride(args.build_event_stride)
     ctx.enable_timing(args.build_events == "timed", only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
     for i in range(args.steps):
@@ -679,6 +683,7 @@ def main():
     if dist:
         dist.barrier()
     build_ms, n_build = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+    ctx.set_timing_stride(1)
     if n_build == 0 and args.build_events == "timed":
         # the steps ran fused (a small --batch, CMPC_STEP_AUTO): the build
         # kernel's own launch time from a build-only pass for the roofline
@@ -1143,6 +1148,7 @@ def main():
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1),
                                 "build_events": args.build_events,
+                                "build_event_stride": args.build_event_stride,
                                 "note": "build: HIP events on every timed step (--build-events timed) or "
                                         "in a later pass of the same steps (separate); iterate: events in "
                                         "a second pass of the same step loop after the timed steps"},

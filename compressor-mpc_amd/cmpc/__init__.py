@@ -377,6 +377,10 @@ class Context:
                 flag |= 2 << k
         check(self.lib.cmpc_enable_timing(self._h, flag), "enable_timing")
 
+    def set_timing_stride(self, stride: int):
+        """Time only every stride-th launch of each timed kernel."""
+        check(self.lib.cmpc_set_timing_stride(self._h, int(stride)), "cmpc_set_timing_stride")
+
     def kernel_time(self, kernel: int):
         ms = ctypes.c_double()
         n = ctypes.c_int64()

@@ -96,7 +96,7 @@ EXPORTS = (
     "cmpc_set_reference", "cmpc_set_state", "cmpc_get_state", "cmpc_upload_lin",
     "cmpc_lin_device", "cmpc_build", "cmpc_set_build_variant", "cmpc_rows_lds_model", "cmpc_last_build_kernel", "cmpc_set_solve_variant", "cmpc_last_solve_kernel", "cmpc_set_step_variant", "cmpc_last_step_fused", "cmpc_init_warmstart", "cmpc_iterate", "cmpc_step",
     "cmpc_synchronize", "cmpc_download", "cmpc_download_qp", "cmpc_download_trace",
-    "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_plant_dims", "cmpc_plant_default",
+    "cmpc_enable_timing", "cmpc_kernel_time", "cmpc_set_timing_stride", "cmpc_plant_dims", "cmpc_plant_default",
     "cmpc_plant_output", "cmpc_plant_lin_record", "cmpc_qp_solve_batch", "cmpc_qp_solve_batch_map", "cmpc_bind_lin",
     "cmpc_bind_state",
     "cmpc_produce_lin", "cmpc_download_lin", "cmpc_coupled_iterate", "cmpc_coupled_validate",
@@ -170,6 +170,7 @@ def load_library(path: str = LIB_PATH):
         "cmpc_download_qp": ([c_void, P(dbl), P(dbl), P(dbl)], ctypes.c_int),
         "cmpc_download_trace": ([c_void, P(ctypes.c_uint8), P(i32)], ctypes.c_int),
         "cmpc_enable_timing": ([c_void, ctypes.c_int], ctypes.c_int),
+        "cmpc_set_timing_stride": ([c_void, ctypes.c_int], ctypes.c_int),
         "cmpc_kernel_time": ([c_void, ctypes.c_int, P(dbl), P(ctypes.c_int64)], ctypes.c_int),
         "cmpc_plant_dims": ([ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int),
                              P(ctypes.c_int)], ctypes.c_int),

@@ -128,6 +128,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   constexpr int NG = M * NUT + 1;  // gather lanes: QP columns (move k, input c), then z
   constexpr int NDW = ND > 0 ? ND : 1;
   constexpr int U = CMPC_ROWS_U;   // horizon-loop unroll (immediate LDS offsets)
+  static_assert(U == 4 || U == 5 || U == 10, "the unrolled block has 4, 5 or 10 steps");
   static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
   // software-pipelined LDS consumption (CMPC_ROWS_SPLIT, CMPC_ROWS_AS0; round
   // 3) where the registers allow it without scratch: the parallel plant's
@@ -571,15 +572,22 @@ void cmpc_build_rows_kernel(BuildParams P) {
 #if CMPC_ROWS_U >= 5
         CMPC_ROWS_STEP(4)
 #endif
+#if CMPC_ROWS_U >= 10
+        CMPC_ROWS_STEP(5)
+        CMPC_ROWS_STEP(6)
+        CMPC_ROWS_STEP(7)
+        CMPC_ROWS_STEP(8)
+        CMPC_ROWS_STEP(9)
+#endif
         CMPC_ROWS_TAIL()
         wq += U * winc;
         rq += U * rinc;
         yp += U * yinc;
       }
-      // a remainder of two or three steps starts with a two-step block: its
+      // a remainder of two or more steps runs as two-step blocks: their
       // chain registers alternate as in the unrolled loop (a one-step loop
       // copies them back, 11 moves a step)
-      if (U > 2 && r + 2 <= r_end) {
+      while (U > 2 && r + 2 <= r_end) {
         CMPC_ROWS_STEP(0)
         CMPC_ROWS_STEP(1)
         CMPC_ROWS_TAIL()

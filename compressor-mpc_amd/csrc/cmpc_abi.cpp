@@ -202,6 +202,8 @@ struct cmpc_ctx {
   int last_step_fused = 0;
   // timing
   int timing = 0;  // bit k: kernel k (CMPC_KERNEL_*) is timed
+  int timing_stride = 1;                        // time every stride-th launch
+  int64_t timing_seq[CMPC_KERNEL_COUNT] = {};  // launches since cmpc_enable_timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[CMPC_KERNEL_COUNT];
   std::vector<hipEvent_t> event_pool;  // reused so timing stays cheap in a timed loop
   double tot_ms[CMPC_KERNEL_COUNT] = {};
@@ -289,6 +291,7 @@ class TimedLaunch {
   int begin() {
     cmpc_launch_events = LaunchEvents{};
     if (!((c_->timing >> k_) & 1)) return 0;
+    if (c_->timing_seq[k_]++ % c_->timing_stride) return 0;  // a sampled launch only
     HIP_TRY(pooled_event(c_, &e0_));
     HIP_TRY(pooled_event(c_, &e1_));
     cmpc_launch_events.start = e0_;
@@ -2056,7 +2059,15 @@ int cmpc_enable_timing(cmpc_ctx* c, int enable) {
   for (int k = 0; k < CMPC_KERNEL_COUNT; ++k) {
     c->tot_ms[k] = 0;
     c->launches[k] = 0;
+    c->timing_seq[k] = 0;
   }
+  return 0;
+}
+
+int cmpc_set_timing_stride(cmpc_ctx* c, int stride) {
+  if (!c) return fail("null context");
+  if (stride < 1) return fail("cmpc_set_timing_stride: stride must be >= 1");
+  c->timing_stride = stride;
   return 0;
 }
 

@@ -252,7 +252,7 @@ double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave)
       tail();
       advance(U);
     }
-    if (U > 2 && r + 2 <= r_end) {  // the kernel's two-step remainder block
+    while (U > 2 && r + 2 <= r_end) {  // the kernel's two-step remainder blocks
       step(0);
       step(1);
       tail();

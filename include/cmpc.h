@@ -242,6 +242,11 @@ int cmpc_download_trace(cmpc_ctx* ctx, uint8_t* trace, int32_t* ntrace);
 int cmpc_enable_timing(cmpc_ctx* ctx, int enable);
 int cmpc_kernel_time(cmpc_ctx* ctx, int kernel, double* total_ms,
                      int64_t* launches);
+/* Time only every stride-th launch of each timed kernel (1, the default:
+ * every launch).  An event-stamped launch costs the stream a few us after
+ * the kernel; sampling keeps the mean launch time while the untimed launches
+ * run as in production.  Counted from the last cmpc_enable_timing. */
+int cmpc_set_timing_stride(cmpc_ctx* ctx, int stride);
 
 /* The batched QP solver alone, on device `device`, for host arrays of nqp
  * QPs of size n (nu inputs per move): H nqp*n*n, g/lb/ub/lbA/ubA nqp*n,

@@ -208,7 +208,7 @@ def simulate(d, L, wave=0, verbose=False):
             for ln in lanes:
                 ln["wq"] += U * ln["winc"]; ln["rq"] += U * ln["rinc"]; ln["yp"] += U * ln["yinc"]
             r += U
-        if U > 2 and r + 2 <= r_end:  # the kernel's two-step remainder block
+        while U > 2 and r + 2 <= r_end:  # the kernel's two-step remainder blocks
             step(0)
             step(1)
             tail()

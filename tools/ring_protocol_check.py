@@ -81,7 +81,7 @@ def check(p, D, M=2, U=KERNEL_U):
                 if rq[k] is not None:
                     rq[k] += U * rinc[k]
             r += U
-        if U > 2 and r + 2 <= r_end:  # the two-step remainder block
+        while U > 2 and r + 2 <= r_end:  # the two-step remainder blocks
             step(0)
             step(1)
             if wq is not None:
