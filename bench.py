@@ -504,11 +504,21 @@ def spawn_ranks(n: int, argv, script=None) -> int:
     env = dict(os.environ)
     env[SELF_LAUNCH_ENV] = "1"
     log("bench.py: starting " + " ".join(cmd[1:]))
+    import signal
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
-    for line in p.stdout:
-        sys.stdout.write(line)
-        sys.stdout.flush()
-    return p.wait()
+
+    def forward(signum, _frame):  # a time limit on this process reaches the ranks
+        p.send_signal(signum)
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for line in p.stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        return p.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
 
 
 def main():

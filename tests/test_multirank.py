@@ -313,3 +313,37 @@ def test_bench_spawn_ranks_relays_rank0_and_exit_code(tmp_path, capfd):
     d = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
     assert d == {"world": 2, "argv": ["--gpus", "2"], "marker": "1"}
     assert b.spawn_ranks(2, ["--fail"], script=str(script)) != 0
+
+
+def test_bench_spawn_ranks_forwards_termination(tmp_path):
+    """A time limit on `bench.py --gpus N` (SIGTERM to the parent) reaches the
+    torch.distributed.run child and its ranks: the parent returns promptly
+    instead of leaving ranks behind."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "rank.py"
+    pidfile = tmp_path / "pids"
+    script.write_text("import os, time\n"
+                      f"open({str(pidfile)!r} + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+                      "time.sleep(600)\n")
+    driver = ("import importlib.util, sys\n"
+              f"spec = importlib.util.spec_from_file_location('b', {os.path.join(root, 'bench.py')!r})\n"
+              "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+              f"sys.exit(b.spawn_ranks(2, [], script={str(script)!r}))\n")
+    p = subprocess.Popen([sys.executable, "-c", driver])
+    t0 = time.time()
+    while not all(os.path.exists(f"{pidfile}{r}") for r in range(2)):
+        assert time.time() - t0 < 120 and p.poll() is None
+        time.sleep(0.2)
+    ranks = [int(open(f"{pidfile}{r}").read()) for r in range(2)]
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    assert p.returncode != 0
+    t1 = time.time()
+    while any(os.path.exists(f"/proc/{pid}") and "zombie" not in open(f"/proc/{pid}/status").read().lower()
+              for pid in ranks):
+        assert time.time() - t1 < 30, "a rank outlived the terminated parent"
+        time.sleep(0.2)
