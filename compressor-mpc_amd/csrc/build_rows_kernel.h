@@ -127,7 +127,7 @@ void cmpc_build_rows_kernel(BuildParams P) {
   constexpr int NV = NU * M;
   constexpr int NG = M * NUT + 1;  // gather lanes: QP columns (move k, input c), then z
   constexpr int NDW = ND > 0 ? ND : 1;
-  constexpr int U = CMPC_ROWS_U;   // horizon-loop unroll (immediate LDS offsets)
+  constexpr int U = cmpc_rows_unroll(NY);  // horizon-loop unroll (immediate LDS offsets)
   static_assert(U == 4 || U == 5 || U == 10, "the unrolled block has 4, 5 or 10 steps");
   static_assert(M == 1 || M == 2, "the ring hand-off holds one step of history");
   // software-pipelined LDS consumption (CMPC_ROWS_SPLIT, CMPC_ROWS_AS0; round
@@ -569,16 +569,14 @@ void cmpc_build_rows_kernel(BuildParams P) {
         CMPC_ROWS_STEP(1)
         CMPC_ROWS_STEP(2)
         CMPC_ROWS_STEP(3)
-#if CMPC_ROWS_U >= 5
-        CMPC_ROWS_STEP(4)
-#endif
-#if CMPC_ROWS_U >= 10
-        CMPC_ROWS_STEP(5)
-        CMPC_ROWS_STEP(6)
-        CMPC_ROWS_STEP(7)
-        CMPC_ROWS_STEP(8)
-        CMPC_ROWS_STEP(9)
-#endif
+        if constexpr (U >= 5) CMPC_ROWS_STEP(4)
+        if constexpr (U >= 10) {
+          CMPC_ROWS_STEP(5)
+          CMPC_ROWS_STEP(6)
+          CMPC_ROWS_STEP(7)
+          CMPC_ROWS_STEP(8)
+          CMPC_ROWS_STEP(9)
+        }
         CMPC_ROWS_TAIL()
         wq += U * winc;
         rq += U * rinc;

@@ -78,6 +78,12 @@ inline void cmpc_allow_lds(const void* kernel, size_t bytes) {
 #ifndef CMPC_ROWS_U
 #define CMPC_ROWS_U 5            // horizon unroll of the row build kernel (4 or 5; 5: p = 50 in whole blocks, +0.7%)
 #endif
+#ifndef CMPC_ROWS_U2
+#define CMPC_ROWS_U2 10          // ... for ny = 2 (config 3: 211 -> 205 us; profiles/r6f_stride_u10_ab/)
+#endif
+// the row build kernel's horizon unroll for ny outputs (the kernel and its
+// LDS layout, rows_layout.cpp, take it from here)
+__host__ __device__ constexpr int cmpc_rows_unroll(int ny) { return ny == 2 ? CMPC_ROWS_U2 : CMPC_ROWS_U; }
 #define CMPC_ROWS_NSEG 16        // loop segment bounds of the row build kernel
 #define CMPC_REC_CHUNKS 3        // 16-byte lin-record chunks per lane (rec_len <= 384)
 // QPs (= lanes) per solve workgroup: one wave, so a batch of fewer waves than
@@ -121,6 +127,7 @@ struct RowsLayout {
   int ring[CMPC_MAX_INPUTS];      // entries of a wrapping delayed line, 0: a plain line
   int ch_off, w_off, WL;
   int nseg, seg[CMPC_ROWS_NSEG];  // ascending distinct D, p - D and wrap steps inside (0, p)
+  int U;                          // the kernel's horizon unroll (cmpc_rows_unroll)
 };
 
 struct SolveParams {

@@ -30,7 +30,7 @@
 
 namespace {
 
-constexpr int kU = CMPC_ROWS_U;   // horizon unroll of the kernel (U in build_rows.hip)
+
 constexpr int kLdsBytes = 160 * 1024;
 
 struct Pads {
@@ -54,7 +54,7 @@ int rows_ring_reader_wrap(int R, int D, int M, int k) { return R + D - (M - 1 - 
 // bytes per workgroup.
 size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, RowsLayout* R) {
   std::memset(R, 0, sizeof *R);
-  const int M = d.m, ny = d.ny, U = kU;
+  const int M = d.m, ny = d.ny, U = cmpc_rows_unroll(d.ny);
   int o = 0;
   for (int i = 0; i < d.nu_tot; ++i) {
     const int c = pd.order[i];
@@ -79,6 +79,7 @@ size_t make_layout(const cmpc_dims& d, int nd, int rec_len, const Pads& pd, Rows
   R->zr_off = o;
   o += U * ny;
   R->LQ = up(o, 2) + 2 * pd.LQ;
+  R->U = U;
   // the C_hat rows overlay the hand-off areas when those are large enough
   // (build_rows.hip reads them in the prologue, before any area is written)
   const int chs = 4 * ny * 16;
@@ -143,7 +144,7 @@ int group_cycles(const int* a, const bool* act, int g0, int n, int nbank) {
 // Extra LDS cycles per wave-step of the horizon loop for wave `wave`; the
 // per-lane pointer arithmetic is the kernel's (build_rows.hip).
 double loop_conflicts(const cmpc_dims& d, int nd, const RowsLayout& R, int wave) {
-  const int NS = d.ns, NY = d.ny, NUT = d.nu_tot, M = d.m, ND = nd, S = d.S, p = d.p, U = kU;
+  const int NS = d.ns, NY = d.ny, NUT = d.nu_tot, M = d.m, ND = nd, S = d.S, p = d.p, U = R.U;
   const int NG = M * NUT + 1;
   const int wreg = R.lds_block + wave * R.per_wave;
   int rq[64], rinc[64], rline[64], rsw[64], wq[64], winc[64], wsw[64], dump[64], yp[64], yinc[64];

@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     }
     if (4 * R.LQ > R.per_wave || R.w_off + 4 * L.nd * R.WL > R.per_wave)
       return fail("regions outside the wave's LDS", d);
-    if (R.dump_off + CMPC_ROWS_U * d.ny > R.LQ || R.zr_off + CMPC_ROWS_U * d.ny > R.LQ)
+    if (R.U != cmpc_rows_unroll(d.ny) || R.dump_off + R.U * d.ny > R.LQ || R.zr_off + R.U * d.ny > R.LQ)
       return fail("dump / zero areas outside the line block", d);
     for (int c = 0; c < d.nu_tot; ++c)
       if (R.lo[c] < 0 || R.lo[c] >= R.LQ) return fail("line offset outside the line block", d);

@@ -184,7 +184,7 @@ def test_row_kernel_ring_protocol_random_delays():
         p = int(rng.integers(2, 260))
         D = int(rng.integers(1, p + 5))
         M = int(rng.integers(1, 3))
-        U = int(rng.choice([rp.KERNEL_U, 4, 5]))
+        U = int(rng.choice([rp.KERNEL_U, 4, 5, 10]))
         errs, ring, _ = rp.check(p, D, M=M, U=U)
         assert errs == 0, (p, D, M, U)
         assert (ring > 0) == ((M - 1) + max(0, p - D) > D + M), (p, D, M)
