@@ -548,9 +548,12 @@ def main():
                          "launch time is the timed launches'); separate: the timed steps run without "
                          "events and the build's launch time comes from a second pass of the same "
                          "steps (A/B of the events' own cost)")
-    ap.add_argument("--build-event-stride", type=int, default=1,
+    ap.add_argument("--build-event-stride", type=int, default=0,
                     help="with --build-events timed: event-stamp every n-th timed build launch only "
-                         "(cmpc_set_timing_stride; the roofline's launch time is the mean of those)")
+                         "(cmpc_set_timing_stride; the roofline's launch time is the mean of those). "
+                         "0 (default): min(5, steps // 4), at least 1, so that >= 4 launches are "
+                         "sampled; an event-stamped launch costs the stream ~4 us after the kernel "
+                         "(every launch stamped: +1.6 %% per step, profiles/r6f_stride_u10_ab/)")
     ap.add_argument("--no-coupled", action="store_true", help="skip the config-4 (coupled) section")
     ap.add_argument("--configs-only", action="store_true",
                     help="only the SURVEY-config section's GPU configs (2, 3, 5), one JSON line: "
@@ -680,7 +683,8 @@ def main():
 
     marker()
     torch.cuda.synchronize()
-    ctx.set_timing_stride(args.build_event_stride)
+    ev_stride = args.build_event_stride or max(1, min(5, args.steps // 4))
+    ctx.set_timing_stride(ev_stride)
     ctx.enable_timing(args.build_events == "timed", only=(cmpc.CMPC_KERNEL_BUILD,))
     t_start = time.perf_counter()
     for i in range(args.steps):
@@ -1136,6 +1140,9 @@ def main():
             "algorithmic_bytes_per_qp": build_bytes(cfg, L),
             "avg_launch_ms": avg_build_s * 1e3,
             "launches": n_build,
+            "launches_note": (f"HIP events (hipExtLaunchKernel) on every {ev_stride}-th build launch of the "
+                              f"{args.steps} timed steps, the mean of those" if args.build_events == "timed"
+                              else "HIP events on every build launch of a second pass of the timed steps"),
         },
         "path_roofline": {
             "definition": ("whole step against the FP64 peak: the FLOPs this build performs per "
@@ -1158,7 +1165,7 @@ def main():
         "kernels_ms_per_step": {"build": build_ms / max(n_build, 1),
                                 "iterate": iter_ms / max(n_iter, 1),
                                 "build_events": args.build_events,
-                                "build_event_stride": args.build_event_stride,
+                                "build_event_stride": ev_stride,
                                 "note": "build: HIP events on every timed step (--build-events timed) or "
                                         "in a later pass of the same steps (separate); iterate: events in "
                                         "a second pass of the same step loop after the timed steps"},
