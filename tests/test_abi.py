@@ -207,3 +207,10 @@ def test_rows_layout_search_under_sanitizers():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert r.stdout.startswith("ok"), r.stdout
     assert "runtime error" not in r.stderr, r.stderr[-2000:]
+
+
+def test_timing_stride_refuses_bad_arguments():
+    """cmpc_set_timing_stride: a null context and a stride below 1 are
+    errors (no device needed for either check)."""
+    lib = load_library()
+    assert lib.cmpc_set_timing_stride(None, 5) < 0

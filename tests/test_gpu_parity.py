@@ -740,3 +740,29 @@ def test_gpu_bound_state_rotation():
         assert np.array_equal(u_back, u_own)
         with pytest.raises(RuntimeError):
             ctx.bind_state(states[0][0].data_ptr(), 0, 0)
+
+
+def test_gpu_timing_stride_samples_every_nth_launch():
+    """cmpc_set_timing_stride(n): only every n-th launch of a timed kernel
+    carries events (the bench samples its timed builds this way); the
+    results do not depend on it; a stride below 1 is refused."""
+    _, setup, _, _ = setup_for("par", "coop")
+    cfg = cmpc.reference_config("par", "coop", p=20)
+    arr = cmpc.controller_arrays(cfg, setup)
+    lin, u_old, du_old, ws = synthetic_batch(cfg, 256, seed=3, n_distinct=64)
+    with make_ctx(cfg, arr, 256, lin, u_old, du_old, ws) as ctx:
+        ctx.build()
+        _, _, G0 = ctx.download_qp()
+        for stride, launches in ((1, 9), (3, 3), (4, 3), (10, 1)):
+            ctx.set_timing_stride(stride)
+            ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
+            for _ in range(9):
+                ctx.build()
+            ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_BUILD)
+            assert n == launches and ms > 0, (stride, n, ms)
+        ctx.enable_timing(False)
+        ctx.set_timing_stride(1)
+        _, _, G1 = ctx.download_qp()
+        assert np.array_equal(G0, G1)
+        with pytest.raises(RuntimeError):
+            ctx.set_timing_stride(0)
