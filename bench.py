@@ -710,7 +710,12 @@ def main():
         ctx.enable_timing(True, only=(cmpc.CMPC_KERNEL_BUILD,))
     t = torch.tensor([elapsed], dtype=torch.float64,
                      device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
+    rank_elapsed = [elapsed]
     if dist:
+        # every rank's own time (the balance of the shards), then the max
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rank_elapsed = [float(x.item()) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
@@ -1110,6 +1115,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed_max / args.steps * 1e3,
+        "rank_ms_per_step": [e / args.steps * 1e3 for e in rank_elapsed],
         "clock_settle": {"seconds": t_settle, "steps": settle_steps,
                          "note": "untimed steps after the warmup, until the clock has ramped up"},
         "higher_is_better": True,

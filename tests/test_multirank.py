@@ -260,6 +260,7 @@ def test_gpu_bench_force_dist_single_rank():
     assert c64["qp_status_ok_fraction"] == 1.0
     assert 0.0 < c64["G_ext_hbm_frac"] < 1.0
     assert d["n_gpus"] == d["gpus_requested"] == 1
+    assert len(d["rank_ms_per_step"]) == 1 and abs(d["rank_ms_per_step"][0] - d["ms_per_step"]) < 1e-9
     # the recorded run's solver load beside the synthetic one
     assert d["recorded_run_working_set_changes_per_qp_step"] == d["recorded_run"]["working_set_changes_per_qp_step"]
     assert d["recorded_run_working_set_changes_per_qp_step"] < d["working_set_changes_per_qp_step"]

@@ -11,7 +11,8 @@ timeout -k 10 400 python3 bench.py --gpus 2 --steps 5 --warmup 2 --batch 16384 -
 rc=$?; echo "dist rc=$rc"; tail -c 400 gpurun_out/dist2.json; echo
 [ $rc -eq 0 ] || exit $rc
 python3 -c "import json,sys; d=json.loads(open('gpurun_out/dist2.json').read().splitlines()[-1]); \
-print('n_gpus', d['n_gpus'], 'launch', d['launch']); sys.exit(0 if d['n_gpus'] == 2 else 1)" || exit 1
+print('n_gpus', d['n_gpus'], 'launch', d['launch'], 'rank_ms_per_step', d['rank_ms_per_step']); \
+sys.exit(0 if d['n_gpus'] == 2 and len(d['rank_ms_per_step']) == 2 else 1)" || exit 1
 timeout -k 10 120 python3 bench.py --gpus 8 --steps 2 --no-cpu > gpurun_out/dist8.json 2> gpurun_out/dist8.err
 rc8=$?; echo "gpus 8 on this box: rc=$rc8 ($(tail -1 gpurun_out/dist8.err))"
 [ $rc8 -ne 0 ] && [ $rc8 -ne 124 ] && [ $rc8 -ne 137 ] || exit 1
