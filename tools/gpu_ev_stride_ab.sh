@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 OUT=gpurun_out/evs_ab.txt; : > $OUT
-for i in 1 2 3; do
+for i in $(seq ${ROUNDS:-3}); do
   for m in s1 s5 s10 sep; do
     case $m in s1) A="--build-event-stride 1";; s5) A="--build-event-stride 5";; s10) A="--build-event-stride 10";; sep) A="--build-events separate";; esac
     timeout -k 10 200 python3 bench.py --headline-only --steps 50 --no-cpu $A > gpurun_out/evs_$m$i.json 2> gpurun_out/evs_$m$i.err || exit $?
