@@ -35,41 +35,17 @@ def coupling_weights(b, s, S_total: int) -> np.ndarray:
     return w[keep].reshape(w.shape[:-1] + (S_total - 1,))
 
 
-GEXT_BLOCK = 64  # CMPC_GEXT_BLOCK (include/cmpc.h)
-
-
-def g_ext_blocked(elem_major: np.ndarray) -> np.ndarray:
-    """[E][nqp] element-major -> the kernel's QP-blocked layout
-    [ceil(nqp / 64)][E][64], flat (the last block zero-padded)."""
-    E, nqp = elem_major.shape
-    nblk = -(-nqp // GEXT_BLOCK)
-    if nqp % GEXT_BLOCK:
-        pad = np.zeros((E, nblk * GEXT_BLOCK), dtype=elem_major.dtype)
-        pad[:, :nqp] = elem_major
-    else:
-        pad = elem_major  # (config 4's 2.1 GB: one copy, the transpose)
-    return np.ascontiguousarray(pad.reshape(E, nblk, GEXT_BLOCK).transpose(1, 0, 2)).reshape(-1)
-
-
-def g_ext_element_major(blocked: np.ndarray, E: int, nqp: int) -> np.ndarray:
-    """The inverse of g_ext_blocked: [E][nqp]."""
-    nblk = -(-nqp // GEXT_BLOCK)
-    b = np.asarray(blocked)[:nblk * E * GEXT_BLOCK].reshape(nblk, E, GEXT_BLOCK)
-    return np.ascontiguousarray(b.transpose(1, 0, 2).reshape(E, nblk * GEXT_BLOCK)[:, :nqp])
-
-
 def synthetic_g_ext(G_local: np.ndarray, S_total: int, S_local: int, s_offset: int,
                     b_offset: int = 0) -> np.ndarray:
-    """G_ext for this rank's QPs (q = b*S_local + local index, scenarios
-    b_offset + b for a tile of the rank's scenarios) in the kernel's
-    QP-blocked layout (g_ext_blocked; g_ext_element_major gives
-    [nV*(S_total-1)*nV][nqp]).  G_local: (nqp, nV, nVo=nV) from the build."""
+    """Element-major G_ext [nV*(S_total-1)*nV][nqp] for this rank's QPs
+    (q = b*S_local + local index, scenarios b_offset + b for a tile of the
+    rank's scenarios).  G_local: (nqp, nV, nVo=nV) from the build."""
     nqp, nV, _ = G_local.shape
     q = np.arange(nqp)
     b, sl = b_offset + q // S_local, q % S_local
     w = coupling_weights(b, s_offset + sl, S_total)            # (nqp, S_total-1)
     out = np.einsum("qj,qav->ajvq", w, G_local)                # (nV, S_total-1, nV, nqp)
-    return g_ext_blocked(out.reshape(nV * (S_total - 1) * nV, nqp))
+    return np.ascontiguousarray(out.reshape(nV * (S_total - 1) * nV, nqp))
 
 
 def others(du_all: np.ndarray, b: int, s: int, S_total: int, S_local: int) -> np.ndarray:

@@ -1848,17 +1848,14 @@ int cmpc_coupled_validate(const cmpc_dims* d, int S_total, int S_local, int s_of
       s_offset + S_local > S_total)
     return fail("cmpc_coupled_iterate: bad S_total / s_offset");
   // every read of the kernel must fall inside the caller's buffers: G_ext
-  // holds nV x (S_total-1) nV per local QP in blocks of CMPC_GEXT_BLOCK QPs
-  // (the last one padded), du_all the plans of all S_total sub-controllers of
-  // the B scenarios (rank-major, S_total / S_local ranks)
+  // holds nV x (S_total-1) nV per local QP, du_all the plans of all S_total
+  // sub-controllers of the B scenarios (rank-major, S_total / S_local ranks)
   const size_t nV = (size_t)L.nV, nqp = (size_t)nqp_ll, B = nqp / (size_t)S_local;
-  const size_t nblk = (nqp + CMPC_GEXT_BLOCK - 1) / CMPC_GEXT_BLOCK;
-  const size_t need_g = nV * (size_t)(S_total - 1) * nV * CMPC_GEXT_BLOCK * nblk;
+  const size_t need_g = nV * (size_t)(S_total - 1) * nV * nqp;
   const size_t need_d = (size_t)S_total * B * nV;
   if (G_ext_len < need_g)
     return fail("cmpc_coupled_iterate: G_ext holds " + std::to_string(G_ext_len) + " doubles, the kernel reads " +
-                std::to_string(need_g) + " (nV*(S_total-1)*nV per local QP, in blocks of " +
-                std::to_string(CMPC_GEXT_BLOCK) + " QPs)");
+                std::to_string(need_g) + " (nV*(S_total-1)*nV per local QP)");
   if (du_all_len < need_d)
     return fail("cmpc_coupled_iterate: du_all holds " + std::to_string(du_all_len) + " doubles, the kernel reads " +
                 std::to_string(need_d) + " (S_total x B x nV: every rank's plans; does S_local x world cover "

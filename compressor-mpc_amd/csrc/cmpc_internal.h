@@ -285,7 +285,7 @@ struct CoupledParams {
   double* du;             // nqp * nV (context buffer)
   double* du_out;         // nqp * nV caller buffer (the next all-gather's input) or null
   int32_t *status, *nwsr;
-  const double* G_ext;    // [nqp / 64][nV * (S_total-1) * nV][64], QP-blocked (include/cmpc.h)
+  const double* G_ext;    // [nV * (S_total-1) * nV][nqp], element-major
   const double* du_all;   // [world][B][S_local][nV], all-gathered plans
   int nqp, qp_len, nu_tot, S_cfg, S_total, S_local, s_offset, B;
   uint32_t flags;

@@ -7,11 +7,8 @@
 //                                  with du_other = all other sub-controllers' plans in
 //                                  global order, nerve_center.h:280-285)
 //   du  = SolveQP(H, f_k)         (libs/mpc_qp_solver.cc:42-75), warm-started
-// G_ext (nV x (S_total-1) nV per QP) is stored QP-blocked
-// ([qp / 64][element][qp % 64], include/cmpc.h): the lane-per-QP reads
-// coalesce and a wave streams one contiguous block (element-major
-// [element][qp] rows 2 MiB apart read 0.71 of 8 TB/s, the blocks 0.76:
-// tools/microbench_gext.hip); the gathered plans are rank-major
+// G_ext (nV x (S_total-1) nV per QP) is stored element-major ([element][qp]) so
+// the lane-per-QP reads coalesce; the gathered plans are rank-major
 // ([rank][scenario][local sub-controller][nV]), as all_gather_into_tensor
 // lays them out.
 #include <hip/hip_runtime.h>
@@ -71,9 +68,8 @@ void cmpc_coupled_kernel(CoupledParams P) {
   double fk[N];
 #pragma unroll
   for (int a = 0; a < N; ++a) fk[a] = f[a];
-  constexpr int GB = CMPC_GEXT_BLOCK;
-  const size_t rs = (size_t)N * GB;  // stride of one column block (N elements of G_ext)
-  const double* gq = P.G_ext + ((size_t)(q / GB) * N * nvo) * GB + (q % GB);
+  const size_t rs = (size_t)N * P.nqp;  // stride of one column block (N rows of G_ext)
+  const double* gq = P.G_ext + q;
 #pragma unroll 4
   for (int jj = 0; jj < P.S_total - 1; ++jj) {
     const int j = jj < sg ? jj : jj + 1;
@@ -86,7 +82,7 @@ void cmpc_coupled_kernel(CoupledParams P) {
     for (int a = 0; a < N; ++a)
 #pragma unroll
       for (int v = 0; v < N; ++v)
-        fk[a] = fk[a] + gq[(size_t)a * nvo * GB + jj * rs + (size_t)v * GB] * d[v];
+        fk[a] = fk[a] + gq[(size_t)a * nvo * P.nqp + jj * rs + (size_t)v * P.nqp] * d[v];
   }
 
   double x[N];

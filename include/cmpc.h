@@ -312,8 +312,6 @@ int cmpc_get_input_host(cmpc_ctx* ctx, const double* du_last, uint32_t flags);
 int cmpc_update_u(cmpc_ctx* ctx, const double* du_full);
 int cmpc_update_u_host(cmpc_ctx* ctx, const double* du_full);
 
-#define CMPC_GEXT_BLOCK 64 /* QPs per block of the coupled iteration's G_ext */
-
 /* Sub-controller-sharded cooperative iteration.
  * S_total sub-controllers per scenario are spread over the ranks, S_local of
  * them on this context (QP slot q = scenario * S_local + local index; global
@@ -321,19 +319,13 @@ int cmpc_update_u_host(cmpc_ctx* ctx, const double* du_full);
  * One Jacobi iteration (nerve_center.h:146-172 with ApplyOtherInput
  * distributed_solver.h:98-103):
  *   f_k = f + G_ext du_other,   du = SolveQP(H, f_k) warm-started
- * G_ext: device, QP-blocked: [ceil(B*S_local / 64)][nV * (S_total-1) * nV][64],
- *        element e of local QP q at ((q / 64) * E + e) * 64 + q % 64, E =
- *        nV * (S_total-1) * nV (the last block padded to 64 QPs); within a
- *        QP's E elements, row a of column block j (the j-th other
- *        sub-controller in global order), entry v, is e = a * (S_total-1) * nV
- *        + j * nV + v.  A wave's 64 QPs read one contiguous block (an
- *        element-major [E][B*S_local] layout read 0.71 of 8 TB/s, this one
- *        0.76: tools/microbench_gext.hip).
+ * G_ext: device, [nV * (S_total-1) * nV][B*S_local] (element-major),
+ *        column block j = the j-th other sub-controller in global order.
  * du_all: device, all-gathered plans [world][B][S_local][nV] (rank-major),
  *        world = S_total / S_local: the kernel reads all of it.
  * G_ext_len, du_all_len: the element counts (doubles) of the caller's two
  *        buffers.  The call is refused (-1, cmpc_last_error) unless
- *        G_ext_len >= nV*(S_total-1)*nV * 64 * ceil(B*S_local / 64) and
+ *        G_ext_len >= nV*(S_total-1)*nV * B*S_local and
  *        du_all_len >= S_total * B * nV, i.e. unless every read of the
  *        kernel falls inside them (a rank layout that does not cover
  *        S_total would otherwise read past the gathered plans).

@@ -15,36 +15,12 @@ import pytest
 import torch.multiprocessing as mp
 
 import _oracle as O
-from cmpc.coupled import (GEXT_BLOCK, coupled_jacobi, coupling_weights, g_ext_blocked, g_ext_element_major,
-                          others, synthetic_g_ext)
+from cmpc.coupled import coupled_jacobi, coupling_weights, others, synthetic_g_ext
 
 S_TOTAL, B, K = 8, 6, 9
 # SURVEY config 4's real partition (8 ranks x 8 sub-controllers), rehearsed on
 # CPU with a small batch
 S_TOTAL8, B8 = 64, 2
-
-
-def g_elem(G_local, S_total, sl, off):
-    """synthetic_g_ext in element-major form [nV*(S_total-1)*nV][nqp]."""
-    nqp, nV = G_local.shape[0], G_local.shape[1]
-    return g_ext_element_major(synthetic_g_ext(G_local, S_total, sl, off), nV * (S_total - 1) * nV, nqp)
-
-
-def test_g_ext_blocked_layout():
-    """The kernel's QP-blocked G_ext (include/cmpc.h): element e of QP q at
-    ((q // 64) * E + e) * 64 + q % 64, the last block zero-padded; the
-    inverse recovers the element-major array, for ragged QP counts too."""
-    rng = np.random.default_rng(5)
-    for E, nqp in ((12, 1), (12, 64), (1008, 130), (16, 200)):
-        em = rng.normal(size=(E, nqp))
-        bl = g_ext_blocked(em)
-        nblk = -(-nqp // GEXT_BLOCK)
-        assert bl.shape == (nblk * E * GEXT_BLOCK,)
-        q = rng.integers(0, nqp, 50)
-        e = rng.integers(0, E, 50)
-        assert np.array_equal(bl[((q // 64) * E + e) * 64 + q % 64], em[e, q])
-        assert np.array_equal(g_ext_element_major(bl, E, nqp), em)
-        assert not bl.reshape(nblk, E, 64)[-1][:, nqp - (nblk - 1) * 64:].any()
 
 
 def test_coupling_weights_are_layout_independent():
@@ -53,12 +29,12 @@ def test_coupling_weights_are_layout_independent():
     assert np.all(w > 0) and w.max() <= 0.6
     # the same (scenario, s, j) triple gives the same weight in any sharding
     G = np.random.default_rng(0).normal(size=(B * S_TOTAL, 4, 4))
-    full = g_elem(G, S_TOTAL, S_TOTAL, 0).reshape(4, (S_TOTAL - 1) * 4, B, S_TOTAL)
+    full = synthetic_g_ext(G, S_TOTAL, S_TOTAL, 0).reshape(4, (S_TOTAL - 1) * 4, B, S_TOTAL)
     for world in (2, 4):
         sl = S_TOTAL // world
         for r in range(world):
             Gr = G.reshape(B, S_TOTAL, 4, 4)[:, r * sl:(r + 1) * sl].reshape(-1, 4, 4)
-            part = g_elem(Gr, S_TOTAL, sl, r * sl).reshape(4, (S_TOTAL - 1) * 4, B, sl)
+            part = synthetic_g_ext(Gr, S_TOTAL, sl, r * sl).reshape(4, (S_TOTAL - 1) * 4, B, sl)
             assert np.array_equal(part, full[:, :, :, r * sl:(r + 1) * sl])
 
 
@@ -94,7 +70,7 @@ def oracle_loop(cfg, arr, H, f, G, u_old, rank, world, gather, S_total=S_TOTAL, 
     """This rank's QPs through coupled_jacobi with or_qp_solve (the oracle)."""
     sl = S_total // world
     glob = [b * S_total + rank * sl + i for b in range(Bn) for i in range(sl)]
-    Gx = g_elem(G[glob], S_total, sl, rank * sl).reshape(4, -1, len(glob))
+    Gx = synthetic_g_ext(G[glob], S_total, sl, rank * sl).reshape(4, -1, len(glob))
     ws = np.zeros(len(glob), np.uint32)
     nu = cfg.nu
 
@@ -200,7 +176,7 @@ def test_abi_refuses_coupled_reads_beyond_the_callers_buffers():
     nqp = Bsc * S_local
     dims = CmpcDims.from_config(cfg, nqp // cfg.S)
     nV = cfg.nV
-    g_len = nV * 63 * nV * nqp  # nqp = 32 768: whole blocks of 64
+    g_len = nV * 63 * nV * nqp
     one_rank = nqp * nV
     rc = lib.cmpc_coupled_validate(ctypes.byref(dims), 64, S_local, 0, g_len, one_rank)
     assert rc == -1
@@ -349,7 +325,7 @@ def test_gpu_config4_full_size_matches_oracle():
         ctx.upload_lin(lin)
         ctx.build()
         H, f, G = ctx.download_qp()
-        Gx_host = synthetic_g_ext(G, S_total, S_total, 0)           # QP-blocked
+        Gx_host = synthetic_g_ext(G, S_total, S_total, 0)           # (4 * 63 * 4, nqp)
         Gx = torch.from_numpy(Gx_host).cuda()
         cr = CoupledRank(ctx, S_total, S_total, 0, 1, Gx)
         cr.step(K4)
@@ -366,7 +342,7 @@ def test_gpu_config4_full_size_matches_oracle():
     # sample's QPs, the kernel's summation order j, then a, then v)
     sample = np.linspace(0, Bsc - 1, 16).astype(int)
     qs = (sample[:, None] * S_total + np.arange(S_total)[None, :]).reshape(-1)
-    G3 = g_ext_element_major(Gx_host, 4 * (S_total - 1) * 4, nqp).reshape(4, (S_total - 1) * 4, nqp)[:, :, qs]
+    G3 = Gx_host.reshape(4, (S_total - 1) * 4, nqp)[:, :, qs]      # (4, 252, nq_s)
     nu = cfg.nu
     ws = np.zeros(len(qs), np.uint32)
     st_o = np.zeros(len(qs), np.int32)
