@@ -12,7 +12,7 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
 
 
 def main():

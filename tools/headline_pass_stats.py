@@ -21,7 +21,9 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+    """The kernel's name without its signature: rocprofv3 -T already
+    truncates; full names may carry a "(anonymous namespace)::" prefix."""
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
 
 
 def last_line(path):
