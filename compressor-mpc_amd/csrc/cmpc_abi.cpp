@@ -1083,15 +1083,26 @@ int cmpc_control_step_download(cmpc_ctx* c, const double* u_full, const double* 
   if (stage_host(c, h, n, 2, d)) return -1;
   bool flagged = false;
   const int rc = control_step(c, d[0], d[1], K, &flagged);
-  if (stage_done(c) || rc) return -1;
-  if (!flagged || !c->out_host) return cmpc_download(c, du, status, nwsr);
+  if (rc) {
+    (void)stage_done(c);
+    return -1;
+  }
+  if (!flagged || !c->out_host) {
+    if (stage_done(c)) return -1;
+    return cmpc_download(c, du, status, nwsr);
+  }
+  // polled: the kernel stores the done word after its last read of the
+  // staged inputs, so once the word is seen the staging buffer is free and
+  // no event need guard it (an event record and its wait cost ~1 us per call)
   const volatile uint32_t* w = c->done_host;
   const uint32_t want = c->done_seq;
   const auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (__atomic_load_n(const_cast<const uint32_t*>(w), __ATOMIC_ACQUIRE) != want) {
-    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1))
+    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      if (stage_done(c)) return -1;
       return cmpc_download(c, du, status, nwsr);  // (the stream synchronisation path)
+    }
   }
   const size_t nq = (size_t)c->nqp;
   if (du) std::memcpy(du, c->out_block, sizeof(double) * nq * c->L.nV);
