@@ -787,7 +787,8 @@ __device__ __forceinline__ void build_wave_body(const BuildParams& P) {
   // 4 epilogue, 5 back-edge; 6 QPs, 7 marker, 8-11 clocks, 12-14 placement
   if (lane == 0) {
     const uint64_t t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
-    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + wave) * 16;
+    // (the hardware wave: SPLIT's two waves of a QP slot write their own)
+    double* dbg = P.qp + (size_t)(blockIdx.x * CMPC_BUILD_WAVES + (threadIdx.x >> 6)) * 16;
     for (int i = 0; i < 6; ++i) dbg[i] = (double)tsum[i];
     dbg[6] = done_qp;
     dbg[7] = 1.0;
