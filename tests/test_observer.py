@@ -415,6 +415,51 @@ def test_gpu_control_step_equals_three_calls(plant, ctype, p, B, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("plant,ctype,p,B,K", [
+    ("par", "coop", 50, 1, 9),     # the reference's own call pattern (polled)
+    ("ser", "cent", 100, 1, 1),    # SURVEY config 1 at B = 1 (polled)
+    ("par", "coop", 20, 3, 9)])    # two workgroups: the stream-synchronised path
+def test_gpu_polled_control_steps_back_to_back(plant, ctype, p, B, K):
+    """cmpc_control_step_download called back to back with a new y every call
+    and nothing else in between: the polled call frees the page-locked
+    staging buffer of its inputs once the kernel's done word is seen (no
+    event), so the next call's inputs may overwrite it at once.  Every call's
+    plans, statuses and nWSR equal the three-call path's bit for bit."""
+    cfg, arr, dims, L, rng, x, u, y, M = setup(plant, ctype, p, B, 23, xs=1e-4, us=1e-3, ms=0.01)
+    nq = B * cfg.S
+    T = 24
+    ys = [y * (1 + 3e-4 * rng.normal(size=y.shape)) for _ in range(T)]
+    out = []
+    for polled in (False, True):
+        with cmpc.Context(cfg, B, device=0) as ctx:
+            ctx.configure(arr)
+            ctx.set_state(np.zeros((nq, cfg.nu_tot)), np.zeros((nq, cfg.nV)), np.zeros(nq, np.uint32))
+            for s_ in range(cfg.S):
+                ctx.set_observer(s_, M[s_])
+            tx, tu = dev(x), dev(u)
+            ctx.observer_init(tx.data_ptr(), tu.data_ptr(), dev(y).data_ptr())
+            ctx.build()
+            ctx.init_warmstart()
+            res = []
+            if polled:
+                for t in range(T):
+                    res.append(tuple(np.array(a, copy=True) for a in ctx.control_step_download(u, ys[t], K)))
+                    assert ctx.last_step_fused() == 1
+            else:
+                tys = [dev(a) for a in ys]
+                for t in range(T):
+                    ctx.observe_step(tu.data_ptr(), tys[t].data_ptr())
+                    ctx.step(K, 0)
+                    ctx.observe_apply()
+                    res.append(ctx.download())
+            out.append(res)
+    for t, (a, b) in enumerate(zip(*out)):
+        for i, (va, vb) in enumerate(zip(a, b)):
+            assert np.array_equal(va, vb), (t, i)
+    assert any(not np.array_equal(out[1][t][0], out[1][t + 1][0]) for t in range(T - 1))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", GC.NAMES)
 def test_gpu_step0_golden_through_observer(name):
     """Initialize + GenerateInitialQP through the observer path reproduce the
