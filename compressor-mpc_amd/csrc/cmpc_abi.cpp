@@ -1087,22 +1087,25 @@ int cmpc_control_step_download(cmpc_ctx* c, const double* u_full, const double* 
     (void)stage_done(c);
     return -1;
   }
-  if (!flagged || !c->out_host) {
-    if (stage_done(c)) return -1;
-    return cmpc_download(c, du, status, nwsr);
-  }
+  // (after cmpc_download's stream synchronisation the kernels have read the
+  // staged inputs too: no event is needed on that path either)
+  auto synced = [&]() {
+    if (cmpc_download(c, du, status, nwsr) == 0) return 0;
+    (void)stage_done(c);
+    return -1;
+  };
+  if (!flagged || !c->out_host) return synced();
   // polled: the kernel stores the done word after its last read of the
   // staged inputs, so once the word is seen the staging buffer is free and
-  // no event need guard it (an event record and its wait cost ~1 us per call)
+  // no event need guard it (its record and the next call's wait on it cost
+  // ~5 us per B = 1 call: profiles/r6q_b1_noevent_ab.txt)
   const volatile uint32_t* w = c->done_host;
   const uint32_t want = c->done_seq;
   const auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (__atomic_load_n(const_cast<const uint32_t*>(w), __ATOMIC_ACQUIRE) != want) {
-    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-      if (stage_done(c)) return -1;
-      return cmpc_download(c, du, status, nwsr);  // (the stream synchronisation path)
-    }
+    if ((++spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1))
+      return synced();  // (the stream synchronisation path)
   }
   const size_t nq = (size_t)c->nqp;
   if (du) std::memcpy(du, c->out_block, sizeof(double) * nq * c->L.nV);
