@@ -1733,11 +1733,13 @@ static int launch_solve(cmpc_ctx* c, const SolveParams& P, const char* who) {
   // AUTO: the row kernel for small batches of nV >= 6 QPs (centralized: the
   // lane kernel's nV = 8 solve is one long dependency chain per lane, 17 us
   // for one solve of 1 024 QPs against 9 us in rows, tools/time_small.py);
-  // at nV = 4 up to one QP per SIMD (K = 9: 7.7-7.8 vs 9.7-9.9 us from 2 to
-  // 1 024 QPs), the lane kernel above (8 192 QPs: 9.8 vs 16.1 us;
-  // profiles/r5k_small_batch.txt)
+  // at nV = 4 up to four QPs per SIMD (K = 9: 7.7-7.8 vs 9.7-9.9 us from 2
+  // to 1 024 QPs, profiles/r5k_small_batch.txt; in the bench's step loop
+  // with the move applied 9.6-10.2 vs 11.6-12.1 us at 2 048 and 4 096 QPs,
+  // p = 20, profiles/r6r_solver_variant_sweep.txt), the lane kernel above
+  // (8 192 QPs: 11.9 vs 17.5 us)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const bool rows_small = nV >= 6 ? c->nqp < CMPC_SOLVE_ROWS_MAX_QP : c->nqp <= 4 * std::max(c->cus, 1);
+  const bool rows_small = nV >= 6 ? c->nqp < CMPC_SOLVE_ROWS_MAX_QP : c->nqp <= 16 * std::max(c->cus, 1);
   const bool want_rows = c->solve_variant == CMPC_SOLVE_ROWS || (c->solve_variant == CMPC_SOLVE_AUTO && rows_small);
   if (want_rows && cmpc_launch_solve_rows(P, nV, nu, nVo, c->stream) == 0) {
     c->last_solve = CMPC_SOLVE_ROWS;

@@ -185,7 +185,7 @@ int cmpc_last_build_kernel(cmpc_ctx* ctx);
  * 16-lane DPP row, its H^-1 and matrix-vector products spread over the row
  * (batches that leave most SIMDs idle; needs S | 4); CMPC_SOLVE_AUTO
  * (default) rows for nV >= 6 below CMPC_SOLVE_ROWS_MAX_QP QPs and for smaller
- * nV up to one QP per SIMD, where available. */
+ * nV up to four QPs per SIMD, where available. */
 #define CMPC_SOLVE_AUTO 0
 #define CMPC_SOLVE_LANE 1
 #define CMPC_SOLVE_ROWS 2

@@ -97,11 +97,12 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
     ("cent", 16, cmpc.CMPC_SOLVE_ROWS, False), ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, True),
     ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
     ("coop", 1, cmpc.CMPC_SOLVE_ROWS, False), ("coop", 512, cmpc.CMPC_SOLVE_ROWS, False),
+    ("coop", 2048, cmpc.CMPC_SOLVE_ROWS, False),   # 4 096 QPs: four per SIMD
     ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
     ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
 def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
     """CMPC_SOLVE_AUTO: the row solve kernel for nV = 8 batches below 16 384
-    QPs and nV = 4 batches up to one QP per SIMD; CMPC_STEP_AUTO: nV = 8
+    QPs and nV = 4 batches up to four QPs per SIMD; CMPC_STEP_AUTO: nV = 8
     steps fused above one QP per CU and below 16 384 QPs (the one-QP-per-wave
     kernel under one row group per SIMD, the row kernel above), every other
     step the build and the iterate kernel (two launches)."""

@@ -3,7 +3,7 @@ in the bench's step loop (NB resident batches, step i on batch i % NB, build
 + K iterations with the move applied), by the iterate's events, alternating
 from the same snapshot; and the two solvers' plans, statuses and working sets
 compared bit for bit after the loop.  GPU only.
-usage: python tools/solver_variant_ab.py [B ...]"""
+usage: python tools/solver_variant_ab.py [p=P] [B ...]   (horizon P, default 50)"""
 import os
 import sys
 import time
@@ -17,9 +17,11 @@ from cmpc.configs import reference_setup  # noqa: E402
 from cmpc.synthetic import synthetic_batch  # noqa: E402
 
 NB, K, STEPS = 4, 9, 40
-cfg = cmpc.reference_config("par", "coop", p=50)
+args = sys.argv[1:]
+P = int(args.pop(0)[2:]) if args and args[0].startswith("p=") else 50
+cfg = cmpc.reference_config("par", "coop", p=P)
 arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
-for B in [int(a) for a in sys.argv[1:]] or [65536]:
+for B in [int(a) for a in args] or [65536]:
     recs, sts = [], []
     for b in range(NB):
         lin, u, du, w = synthetic_batch(cfg, B, seed=1002 + b, n_distinct=min(B, 2048))
@@ -64,7 +66,7 @@ for B in [int(a) for a in sys.argv[1:]] or [65536]:
             ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
             ctx.enable_timing(False)
             used = ctx.last_solve_kernel()
-            print(f"B {B:6d} round {rnd} {name}: iterate {ms / n * 1e3:7.2f} us (kernel {used})", flush=True)
+            print(f"p {P} B {B:6d} round {rnd} {name}: iterate {ms / n * 1e3:7.2f} us (kernel {used})", flush=True)
             finals[name] = [a.cpu().numpy().copy() for st in sts for a in st]
     same = all(np.array_equal(a.view(np.uint8), b.view(np.uint8)) for a, b in zip(finals["lane"], finals["rows"]))
     print(f"B {B:6d}: states after {STEPS} steps bit-identical between the solvers: {same}", flush=True)
