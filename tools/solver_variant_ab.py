@@ -3,7 +3,7 @@ in the bench's step loop (NB resident batches, step i on batch i % NB, build
 + K iterations with the move applied), by the iterate's events, alternating
 from the same snapshot; and the two solvers' plans, statuses and working sets
 compared bit for bit after the loop.  GPU only.
-usage: python tools/solver_variant_ab.py [p=P] [B ...]   (horizon P, default 50)"""
+usage: python tools/solver_variant_ab.py [p=50] [plant=par] [c=coop] [K=9] [B ...]"""
 import os
 import sys
 import time
@@ -16,11 +16,15 @@ import cmpc  # noqa: E402
 from cmpc.configs import reference_setup  # noqa: E402
 from cmpc.synthetic import synthetic_batch  # noqa: E402
 
-NB, K, STEPS = 4, 9, 40
+NB, STEPS = 4, 40
 args = sys.argv[1:]
-P = int(args.pop(0)[2:]) if args and args[0].startswith("p=") else 50
-cfg = cmpc.reference_config("par", "coop", p=P)
-arr = cmpc.controller_arrays(cfg, reference_setup("par", "coop"))
+opt = {"p": "50", "plant": "par", "c": "coop", "K": "9"}
+while args and "=" in args[0]:
+    k, v = args.pop(0).split("=", 1)
+    opt[k] = v
+P, K = int(opt["p"]), int(opt["K"])
+cfg = cmpc.reference_config(opt["plant"], opt["c"], p=P)
+arr = cmpc.controller_arrays(cfg, reference_setup(opt["plant"], opt["c"]))
 for B in [int(a) for a in args] or [65536]:
     recs, sts = [], []
     for b in range(NB):
@@ -66,7 +70,7 @@ for B in [int(a) for a in args] or [65536]:
             ms, n = ctx.kernel_time(cmpc.CMPC_KERNEL_ITERATE)
             ctx.enable_timing(False)
             used = ctx.last_solve_kernel()
-            print(f"p {P} B {B:6d} round {rnd} {name}: iterate {ms / n * 1e3:7.2f} us (kernel {used})", flush=True)
+            print(f"{opt['plant']}-{opt['c']} p {P} K {K} B {B:6d} round {rnd} {name}: iterate {ms / n * 1e3:7.2f} us (kernel {used})", flush=True)
             finals[name] = [a.cpu().numpy().copy() for st in sts for a in st]
     same = all(np.array_equal(a.view(np.uint8), b.view(np.uint8)) for a, b in zip(finals["lane"], finals["rows"]))
     print(f"B {B:6d}: states after {STEPS} steps bit-identical between the solvers: {same}", flush=True)
