@@ -1943,13 +1943,19 @@ int cmpc_step(cmpc_ctx* c, int K, uint32_t flags) {
   // solver of wave 0 after a workgroup barrier for S = 2, 4), the row kernel
   // from one row group per SIMD up to 16 384 QPs (config 2)
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  // (AUTO fuses nV >= 6 steps above one QP per CU only: below it the
-  // role-split build and the iterate kernel are faster (cent-ser B = 1 21.8 vs
-  // 24.4 us), config 5 (1 024 QPs) fused 37.2 vs 38.4 us with the move; nV = 4
-  // steps are two launches at every size (coop-par 1 024 QPs 17.8 vs 18.6 us,
-  // config 2 26.4 vs 54.1 us; profiles/r5j_split_step_ab.txt,
-  // profiles/r5k_small_batch.txt))
-  const bool auto_fuse = c->nqp < CMPC_SOLVE_ROWS_MAX_QP && c->nqp > std::max(c->cus, 1) && c->L.nV >= 6;
+  // (AUTO fuses nV >= 6 steps from one to four QPs per CU at p >= 50 only:
+  // below one per CU the role-split build and the iterate kernel are faster
+  // (cent-ser B = 1 21.8 vs 24.4 us); in that range fused wins by 2-3 %
+  // (config 5: 37.3 vs 38.1 us with the move; ser-cent p = 100 512 QPs 37.6
+  // vs 38.4 us) but loses at p = 20 (15.0 vs 13.9 us), and above it the split
+  // steps win: 2 048 QPs 17.1 vs 28.3 us (par-cent p = 20) and 60.1 vs 73.0 us
+  // (ser-cent p = 100), 8 192 QPs 112 vs 135 us (par-cent p = 200)
+  // (tools/step_variant_ab.py, profiles/r6r_step_variant_sweep.txt; it costs
+  // 3 % at 4 096 QPs for p = 50 and 200).  nV = 4 steps are two launches at
+  // every size (coop-par 1 024 QPs 17.8 vs 18.6 us, config 2 26.4 vs
+  // 54.1 us; profiles/r5j_split_step_ab.txt, profiles/r5k_small_batch.txt))
+  const int cus1 = std::max(c->cus, 1);
+  const bool auto_fuse = c->L.nV >= 6 && c->nqp > cus1 && c->nqp <= 4 * cus1 && c->d.p >= 50;
   const bool want = c->step_variant == CMPC_STEP_FUSED ||
                     (c->step_variant == CMPC_STEP_AUTO && auto_fuse &&
                      c->build_variant == CMPC_BUILD_AUTO && c->solve_variant == CMPC_SOLVE_AUTO);

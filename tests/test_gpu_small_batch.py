@@ -93,20 +93,21 @@ def test_gpu_row_solver_failure_statuses_equal_lane_solver():
     assert (st == cmpc.CMPC_QP_OK).mean() > 0.9
 
 
-@pytest.mark.parametrize("ctype,B,solve,fused", [
-    ("cent", 16, cmpc.CMPC_SOLVE_ROWS, False), ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, True),
-    ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False),
-    ("coop", 1, cmpc.CMPC_SOLVE_ROWS, False), ("coop", 512, cmpc.CMPC_SOLVE_ROWS, False),
-    ("coop", 2048, cmpc.CMPC_SOLVE_ROWS, False),   # 4 096 QPs: four per SIMD
-    ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False),
-    ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False)])
-def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
+@pytest.mark.parametrize("ctype,B,solve,fused,p", [
+    ("cent", 16, cmpc.CMPC_SOLVE_ROWS, False, 20), ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, False, 20),
+    ("cent", 1024, cmpc.CMPC_SOLVE_ROWS, True, 50), ("cent", 2048, cmpc.CMPC_SOLVE_ROWS, False, 50),
+    ("cent", 65536, cmpc.CMPC_SOLVE_LANE, False, 20),
+    ("coop", 1, cmpc.CMPC_SOLVE_ROWS, False, 20), ("coop", 512, cmpc.CMPC_SOLVE_ROWS, False, 20),
+    ("coop", 2048, cmpc.CMPC_SOLVE_ROWS, False, 20),   # 4 096 QPs: four per SIMD
+    ("coop", 4096, cmpc.CMPC_SOLVE_LANE, False, 20),
+    ("coop", 65536, cmpc.CMPC_SOLVE_LANE, False, 20)])
+def test_gpu_auto_kernel_selection(ctype, B, solve, fused, p):
     """CMPC_SOLVE_AUTO: the row solve kernel for nV = 8 batches below 16 384
     QPs and nV = 4 batches up to four QPs per SIMD; CMPC_STEP_AUTO: nV = 8
-    steps fused above one QP per CU and below 16 384 QPs (the one-QP-per-wave
-    kernel under one row group per SIMD, the row kernel above), every other
-    step the build and the iterate kernel (two launches)."""
-    cfg = cmpc.reference_config("par", ctype, p=20)
+    steps fused from one to four QPs per CU at p >= 50 (the one-QP-per-wave
+    kernel with its row solver), every other step the build and the iterate
+    kernel (two launches)."""
+    cfg = cmpc.reference_config("par", ctype, p=p)
     arr = cmpc.controller_arrays(cfg, reference_setup("par", ctype))
     lin, u, du, ws = synthetic_batch(cfg, B, seed=3, n_distinct=16)
     with cmpc.Context(cfg, B) as ctx:
@@ -123,7 +124,7 @@ def test_gpu_auto_kernel_selection(ctype, B, solve, fused):
             assert ctx.last_solve_kernel() == solve
 
 
-FUSED_CASES = [  # plant, controller, p, K, B scenarios (the kernel AUTO fuses on)
+FUSED_CASES = [  # plant, controller, p, K, B scenarios (pinned to the fused kernels; AUTO fuses config 5)
     ("par", "coop", 20, 9, 4096),     # SURVEY config 2: the row build kernel, lane solver
     ("par", "cent", 20, 1, 8192),     # the row build kernel, row solver per group
     ("par", "coop", 20, 9, 13),       # one-QP-per-wave kernel, lane solver of wave 0
