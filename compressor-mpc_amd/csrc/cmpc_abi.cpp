@@ -962,8 +962,12 @@ static int control_step(cmpc_ctx* c, const double* u_full, const double* y, int 
   if (observer_upload_M(c)) return -1;
   if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
   const cmpc_dims& d = c->d;
+  // one launch up to four QPs per CU: it wins there (config 5's cent-par
+  // p = 200 at 1 024 QPs 50.7 vs 58.6 us, coop-par p = 50 at 512 QPs 48.5 vs
+  // 49.5 us) and loses above (2 048 QPs: 75.2 vs 72.7 and 102.0 vs 73.0 us;
+  // tools/control_step_ab.py, profiles/r6r_control_step_ab.txt)
   const bool fuse = K > 0 && c->step_variant != CMPC_STEP_SPLIT && c->build_variant == CMPC_BUILD_AUTO &&
-                    c->solve_variant == CMPC_SOLVE_AUTO && (c->nqp + 3) / 4 < 4 * std::max(c->cus, 1) &&
+                    c->solve_variant == CMPC_SOLVE_AUTO && c->nqp <= 4 * std::max(c->cus, 1) &&
                     c->L.nuo == (d.S - 1) * d.nu;
   if (fuse) {
     if (ensure_cfg(c)) return -1;

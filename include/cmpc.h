@@ -394,9 +394,9 @@ int cmpc_observer_init_host(cmpc_ctx* ctx, int plant, double p_in, double p_out,
 int cmpc_observe_step_host(cmpc_ctx* ctx, const double* u_full, const double* y);
 /* NerveCenter::GetNextInput (include/nerve_center.h:134-182) on the device:
  * cmpc_observe_step(u_full, y) + cmpc_step(K, 0) + cmpc_observe_apply() with
- * the same results bit for bit, as ONE kernel launch for batches the
- * one-QP-per-wave fused step runs (under one row group per SIMD, AUTO
- * variants, no trace): observer a posteriori + linearisation, the QP build,
+ * the same results bit for bit, as ONE kernel launch for batches of up to
+ * four QPs per CU (AUTO variants, no trace): observer a posteriori +
+ * linearisation, the QP build,
  * K Jacobi iterations and the a-priori update in one workgroup per four QP
  * slots.  Elsewhere the three calls.  Plans, statuses and nWSR through
  * cmpc_download; u_old has moved by the own first moves. */
